@@ -1,0 +1,560 @@
+// capi.hip -- the C ABI of libsdrhip.so (include/sdr_hip.h): contexts,
+// argument validation (every precondition the reference leaves as UB is an
+// SDR_EINVAL here), the host-pointer synchronous wrappers used by the
+// drop-in filter.h implementation, and the device-resident batched calls.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "sdr_common.hpp"
+#include "sdr_hip.h"
+
+struct sdr_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t cur = nullptr;
+  // grow-only device scratch for the host-pointer wrappers and internal use
+  void* buf[10] = {};
+  size_t cap[10] = {};
+  std::string err;
+};
+
+namespace {
+
+enum Slot { kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp };
+
+int fail(sdr_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char msg[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    c->err = msg;
+  }
+  return code;
+}
+
+int hip_fail(sdr_ctx* c, hipError_t e, const char* where) {
+  return fail(c, SDR_EHIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+#define SDR_HIP(ctx, call)                                  \
+  do {                                                      \
+    hipError_t e_ = (call);                                 \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
+  } while (0)
+
+int enter(sdr_ctx* c) {
+  if (!c) return SDR_EINVAL;
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return hip_fail(c, e, "hipSetDevice");
+  return SDR_OK;
+}
+
+void* scratch(sdr_ctx* c, int slot, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (c->cap[slot] >= bytes) return c->buf[slot];
+  if (c->buf[slot]) {
+    (void)hipStreamSynchronize(c->cur);
+    (void)hipFree(c->buf[slot]);
+    c->buf[slot] = nullptr;
+    c->cap[slot] = 0;
+  }
+  size_t want = bytes + bytes / 4;
+  if (hipMalloc(&c->buf[slot], want) != hipSuccess) {
+    c->buf[slot] = nullptr;
+    return nullptr;
+  }
+  c->cap[slot] = want;
+  return c->buf[slot];
+}
+
+// Shared validation of the stateful FIR family (src/filter.cpp:66-83, 123-140).
+int check_fir(sdr_ctx* c, int D, long long n, int nstreams, int ntaps, int ns, const void* x, const void* h,
+              const void* state) {
+  if (!x || !h || !state) return fail(c, SDR_EINVAL, "null pointer");
+  if (D < 1) return fail(c, SDR_EINVAL, "decimation factor %d < 1", D);
+  if (ntaps < 1) return fail(c, SDR_EINVAL, "ntaps %d < 1", ntaps);
+  if (nstreams < 1) return fail(c, SDR_EINVAL, "nstreams %d < 1", nstreams);
+  if (n <= 0) return fail(c, SDR_EINVAL, "empty block");
+  if (n % D != 0)
+    return fail(c, SDR_EINVAL, "block length %lld is not a multiple of %d (reference writes past y, filter.cpp:127-132)",
+                n, D);
+  if (ns < ntaps - 1)
+    return fail(c, SDR_EINVAL, "state length %d < ntaps-1 = %d (reference reads before state, filter.cpp:134)", ns,
+                ntaps - 1);
+  if (n < ns) return fail(c, SDR_EINVAL, "block length %lld < state length %d (filter.cpp:139 state.assign)", n, ns);
+  return SDR_OK;
+}
+
+sdr::FirLaunch fir_args(long long n, int nstreams, int ntaps, int D, int ns) {
+  sdr::FirLaunch a;
+  std::memset(&a, 0, sizeof a);
+  a.n = n;
+  a.nstreams = nstreams;
+  a.ntaps = ntaps;
+  a.D = D;
+  a.ns = ns;
+  return a;
+}
+
+// Vector paths need 16-B aligned bases and strides that keep every stream
+// row aligned; otherwise the generic (scalar) kernel runs -- same results.
+bool vec_ok(const void* p, long long stride_elems, int elem_bytes, int nstreams, int align = 16) {
+  return ((uintptr_t)p % align) == 0 && (nstreams == 1 || ((stride_elems * elem_bytes) % align) == 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sdr_version(void) { return "sdrhip 0.1 (gfx950)"; }
+
+const char* sdr_strerror(int code) {
+  switch (code) {
+    case SDR_OK: return "ok";
+    case SDR_EINVAL: return "invalid argument / reference precondition violated";
+    case SDR_EHIP: return "HIP runtime error";
+    case SDR_ENOMEM: return "device allocation failed";
+    case SDR_ENODEV: return "no such device";
+    default: return "unknown error";
+  }
+}
+
+int sdr_device_count(int* count) {
+  if (!count) return SDR_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return SDR_OK;
+}
+
+int sdr_ctx_create(int device, sdr_ctx** out) {
+  if (!out) return SDR_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SDR_ENODEV;
+  if (hipSetDevice(device) != hipSuccess) return SDR_ENODEV;
+  sdr_ctx* c = new sdr_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SDR_EHIP;
+  }
+  c->cur = c->own;
+  *out = c;
+  return SDR_OK;
+}
+
+int sdr_ctx_destroy(sdr_ctx* c) {
+  if (!c) return SDR_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->cur);
+  for (void* b : c->buf)
+    if (b) (void)hipFree(b);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+  return SDR_OK;
+}
+
+int sdr_ctx_set_stream(sdr_ctx* c, void* s) {
+  if (!c) return SDR_EINVAL;
+  c->cur = s ? static_cast<hipStream_t>(s) : c->own;
+  return SDR_OK;
+}
+
+void* sdr_ctx_get_stream(sdr_ctx* c) { return c ? static_cast<void*>(c->cur) : nullptr; }
+
+int sdr_ctx_synchronize(sdr_ctx* c) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+const char* sdr_ctx_last_error(sdr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int sdr_dev_alloc(sdr_ctx* c, size_t bytes, void** p) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!p) return fail(c, SDR_EINVAL, "null out pointer");
+  if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) return fail(c, SDR_ENOMEM, "hipMalloc(%zu)", bytes);
+  return SDR_OK;
+}
+
+int sdr_dev_free(sdr_ctx* c, void* p) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipFree(p));
+  return SDR_OK;
+}
+
+int sdr_copy_h2d(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->cur));
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+int sdr_copy_d2h(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+int sdr_dev_memset(sdr_ctx* c, void* dst, int value, size_t bytes) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipMemsetAsync(dst, value, bytes, c->cur));
+  return SDR_OK;
+}
+
+// ------------------------------------------------------------ taps (host) --
+// Windowed-sinc design, src/filter.cpp:14-49: the sinc in double, stored to
+// float, then widened again for the sin^2 window and the up-factor gain.
+// Host code (setup, once per run) -- bit-identical to the reference.
+static constexpr double kPi = 3.14159265358979323846;  // include/dy4.h:14
+
+static float window_gain(float tap, int i, int ntaps, int up) {
+  const double s = std::sin((double)i * kPi / (double)ntaps);
+  return (float)((double)tap * (s * s) * (double)(float)up);
+}
+
+int sdr_taps_lpf(float Fs, float Fc, int ntaps, int up, float* h) {
+  if (!h || ntaps < 1 || ntaps > 65535) return SDR_EINVAL;  // filter.h takes unsigned short
+  const int T = ntaps;
+  const double cutoff = (double)(Fc / (Fs / 2));
+  const double centre = ((double)(float)T - 1.0) / 2.0;
+  for (int i = 0; i < T; i++) {
+    float v;
+    if (i == (T - 1) / 2) {
+      v = (float)cutoff;
+    } else {
+      const double arg = kPi * cutoff * ((double)i - centre);
+      v = (float)(cutoff * std::sin(arg) / arg);
+    }
+    h[i] = window_gain(v, i, T, up);
+  }
+  return SDR_OK;
+}
+
+int sdr_taps_bpf(float Fs, float Fb, float Fe, int ntaps, int up, float* h) {
+  if (!h || ntaps < 1 || ntaps > 65535) return SDR_EINVAL;
+  const int T = ntaps;
+  const double centre_f = (double)(((Fe + Fb) / 2) / (Fs / 2));
+  const double pass = (double)((Fe - Fb) / (Fs / 2));
+  const double centre = ((double)(float)T - 1.0) / 2.0;
+  for (int i = 0; i < T; i++) {
+    float v;
+    if (i == (T - 1) / 2) {
+      v = (float)pass;
+    } else {
+      const double arg = kPi * pass / 2 * ((double)i - centre);
+      v = (float)(pass * std::sin(arg) / arg);
+    }
+    v = (float)((double)v * std::cos((double)(i - (T - 1) / 2) * kPi * centre_f));
+    h[i] = window_gain(v, i, T, up);
+  }
+  return SDR_OK;
+}
+
+long long sdr_resample_out_len(int up, int down, long long n) {
+  if (up <= 0 || down <= 0 || n < 0) return -1;
+  const float q = (float)n / (float)down;  // src/filter.cpp:149
+  return (long long)(q * (float)up);
+}
+
+// ------------------------------------------------------ device, batched --
+
+int sdr_fir_decim_f32_dev(sdr_ctx* c, int D, const float* x, long long n, int nstreams, long long x_stride,
+                          const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if ((rc = check_fir(c, D, n, nstreams, ntaps, ns, x, h, state))) return rc;
+  if (!y) return fail(c, SDR_EINVAL, "null output");
+  if (nstreams > 1 && (x_stride < n || y_stride < n / D)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  sdr::FirLaunch a = fir_args(n, nstreams, ntaps, D, ns);
+  a.x0 = x;
+  a.x_stride = x_stride;
+  a.state0 = state;
+  a.y0 = y;
+  a.y_stride = y_stride;
+  const bool fast = vec_ok(x, x_stride, 4, nstreams);  // output alignment is handled in-kernel
+  hipError_t e = sdr::launch_fir(a, h, false, 1, sdr::Src::F32, c->cur, nullptr, nullptr, fast);
+  if (e != hipSuccess) return hip_fail(c, e, "fir_decim launch");
+  return SDR_OK;
+}
+
+int sdr_fir_block_f32_dev(sdr_ctx* c, const float* x, long long n, int nstreams, long long x_stride, const float* h,
+                          int ntaps, float* state, int ns, float* y, long long y_stride) {
+  return sdr_fir_decim_f32_dev(c, 1, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride);
+}
+
+int sdr_fm_demod_f32_dev(sdr_ctx* c, const float* I, const float* Q, long long n, int nstreams, long long stride,
+                         float* prev_i, float* prev_q, float* out, long long out_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!I || !Q || !prev_i || !prev_q || !out) return fail(c, SDR_EINVAL, "null pointer");
+  if (n <= 0) return fail(c, SDR_EINVAL, "empty block (reference reads I[-1], filter.cpp:100)");
+  if (nstreams < 1) return fail(c, SDR_EINVAL, "nstreams < 1");
+  hipError_t e = sdr::launch_demod(I, Q, n, nstreams, stride, prev_i, prev_q, out, out_stride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "demod launch");
+  return SDR_OK;
+}
+
+static int frontend_dev(sdr_ctx* c, sdr::Src src, int D, const float* I, const float* Q, const uint8_t* iq,
+                        long long n, int nstreams, long long x_stride, const float* h, int ntaps, float* state_i,
+                        float* state_q, int ns, float* prev_i, float* prev_q, float* demod, long long out_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  const void* xin = src == sdr::Src::F32 ? (const void*)I : (const void*)iq;
+  if ((rc = check_fir(c, D, n, nstreams, ntaps, ns, xin, h, state_i))) return rc;
+  if (src == sdr::Src::F32 && !Q) return fail(c, SDR_EINVAL, "null Q");
+  if (!state_q || !prev_i || !prev_q || !demod) return fail(c, SDR_EINVAL, "null pointer");
+  const long long nout = n / D;
+  const long long per = src == sdr::Src::F32 ? n : 2 * n;
+  if (nstreams > 1 && (x_stride < per || out_stride < nout)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  sdr::FirLaunch a = fir_args(n, nstreams, ntaps, D, ns);
+  a.x0 = I;
+  a.x1 = Q;
+  a.iq = iq;
+  a.x_stride = x_stride;
+  a.state0 = state_i;
+  a.state1 = state_q;
+  a.prev0 = prev_i;
+  a.prev1 = prev_q;
+  a.out = demod;
+  a.out_stride = out_stride;
+  bool fast;
+  if (src == sdr::Src::F32)
+    fast = vec_ok(I, x_stride, 4, nstreams) && vec_ok(Q, x_stride, 4, nstreams);
+  else
+    fast = vec_ok(iq, x_stride, 1, nstreams, 8);  // 8-B (4-pair) loads
+  float* y0 = nullptr;
+  float* y1 = nullptr;
+  if (!fast || !sdr::fir_has_fast_path(D, ntaps, ns, 2, true, src)) {
+    const size_t bytes = (size_t)nout * (size_t)nstreams * sizeof(float);
+    y0 = static_cast<float*>(scratch(c, kY0, bytes));
+    y1 = static_cast<float*>(scratch(c, kY1, bytes));
+    if (!y0 || !y1) return fail(c, SDR_ENOMEM, "scratch for decimated I/Q (%zu B)", bytes);
+  }
+  hipError_t e = sdr::launch_fir(a, h, true, 2, src, c->cur, y0, y1, fast);
+  if (e != hipSuccess) return hip_fail(c, e, "frontend launch");
+  return SDR_OK;
+}
+
+int sdr_frontend_f32_dev(sdr_ctx* c, int D, const float* I, const float* Q, long long n, int nstreams,
+                         long long x_stride, const float* h, int ntaps, float* state_i, float* state_q, int ns,
+                         float* prev_i, float* prev_q, float* demod, long long out_stride) {
+  return frontend_dev(c, sdr::Src::F32, D, I, Q, nullptr, n, nstreams, x_stride, h, ntaps, state_i, state_q, ns,
+                      prev_i, prev_q, demod, out_stride);
+}
+
+int sdr_frontend_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
+                        const float* h, int ntaps, float* state_i, float* state_q, int ns, float* prev_i,
+                        float* prev_q, float* demod, long long out_stride) {
+  return frontend_dev(c, sdr::Src::U8, D, nullptr, nullptr, iq, npairs, nstreams, iq_stride, h, ntaps, state_i,
+                      state_q, ns, prev_i, prev_q, demod, out_stride);
+}
+
+int sdr_resample_f32_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
+                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
+  if (up < 1 || down < 1) return fail(c, SDR_EINVAL, "up/down factors must be >= 1");
+  if (ntaps < 1 || nstreams < 1 || n <= 0) return fail(c, SDR_EINVAL, "empty taps/streams/block");
+  const long long ny = sdr_resample_out_len(up, down, n);
+  if ((n * up + down - 1) / down > ny)
+    return fail(c, SDR_EINVAL,
+                "n*up/down does not divide: the reference loop writes %lld outputs into %lld (filter.cpp:149-162)",
+                (n * up + down - 1) / down, ny);
+  if ((ntaps - 1) / up > ns)
+    return fail(c, SDR_EINVAL, "state length %d < (ntaps-1)/up = %d (filter.cpp:164)", ns, (ntaps - 1) / up);
+  if (n < ns) return fail(c, SDR_EINVAL, "block length %lld < state length %d (filter.cpp:169)", n, ns);
+  if (nstreams > 1 && (x_stride < n || y_stride < ny)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  if (up == 1) {
+    // identical arithmetic to FIR + decimate by `down` (k = 0..T-1, x[n-k])
+    return sdr_fir_decim_f32_dev(c, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride);
+  }
+  float* hp = static_cast<float*>(scratch(c, kTmp, sdr::resample_scratch_floats(up, ntaps) * sizeof(float)));
+  if (!hp) return fail(c, SDR_ENOMEM, "polyphase table");
+  hipError_t e = sdr::launch_resample(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, hp,
+                                      c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "resample launch");
+  return SDR_OK;
+}
+
+int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
+                        unsigned long long seed) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!iq || npairs <= 0 || nstreams < 1) return fail(c, SDR_EINVAL, "bad synth arguments");
+  hipError_t e = sdr::launch_synth_fm_u8(iq, npairs, nstreams, iq_stride, seed, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "synth launch");
+  return SDR_OK;
+}
+
+int sdr_u8_to_planar_dev(sdr_ctx* c, const uint8_t* iq, long long npairs, int nstreams, long long iq_stride, float* I,
+                         float* Q, long long x_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!iq || !I || !Q || npairs <= 0 || nstreams < 1) return fail(c, SDR_EINVAL, "bad u8_to_planar arguments");
+  if (!vec_ok(iq, iq_stride, 1, nstreams) || !vec_ok(I, x_stride, 4, nstreams) || !vec_ok(Q, x_stride, 4, nstreams))
+    return fail(c, SDR_EINVAL, "u8_to_planar needs 16-B aligned rows");
+  hipError_t e = sdr::launch_u8_to_planar(iq, npairs, nstreams, iq_stride, I, Q, x_stride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "u8_to_planar launch");
+  return SDR_OK;
+}
+
+// -------------------------------------------------- host, synchronous --
+// Each wrapper: copy inputs + state into context scratch, run the device
+// path on one stream, copy outputs + state back, synchronise.
+
+int sdr_fir_decim_f32(sdr_ctx* c, int D, const float* x, long long n, const float* h, int ntaps, float* state, int ns,
+                      float* y) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if ((rc = check_fir(c, D, n, 1, ntaps, ns, x, h, state))) return rc;
+  if (!y) return fail(c, SDR_EINVAL, "null output");
+  const long long nout = n / D;
+  float* dx = static_cast<float*>(scratch(c, kX0, n * sizeof(float)));
+  float* dh = static_cast<float*>(scratch(c, kH, ntaps * sizeof(float)));
+  float* ds = static_cast<float*>(scratch(c, kS0, (ns ? ns : 1) * sizeof(float)));
+  float* dy = static_cast<float*>(scratch(c, kY0, nout * sizeof(float)));
+  if (!dx || !dh || !ds || !dy) return fail(c, SDR_ENOMEM, "scratch");
+  SDR_HIP(c, hipMemcpyAsync(dx, x, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(dh, h, ntaps * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if (ns) SDR_HIP(c, hipMemcpyAsync(ds, state, ns * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if ((rc = sdr_fir_decim_f32_dev(c, D, dx, n, 1, n, dh, ntaps, ds, ns, dy, nout))) return rc;
+  SDR_HIP(c, hipMemcpyAsync(y, dy, nout * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  if (ns) SDR_HIP(c, hipMemcpyAsync(state, ds, ns * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+int sdr_fir_block_f32(sdr_ctx* c, const float* x, long long n, const float* h, int ntaps, float* state, int ns,
+                      float* y) {
+  return sdr_fir_decim_f32(c, 1, x, n, h, ntaps, state, ns, y);
+}
+
+int sdr_resample_f32(sdr_ctx* c, int up, int down, const float* x, long long n, const float* h, int ntaps,
+                     float* state, int ns, float* y, long long y_cap) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
+  const long long ny = sdr_resample_out_len(up, down, n);
+  if (ny < 0) return fail(c, SDR_EINVAL, "bad up/down");
+  if (y_cap < ny) return fail(c, SDR_EINVAL, "output capacity %lld < %lld", y_cap, ny);
+  float* dx = static_cast<float*>(scratch(c, kX0, (n > 0 ? n : 1) * sizeof(float)));
+  float* dh = static_cast<float*>(scratch(c, kH, ntaps * sizeof(float)));
+  float* ds = static_cast<float*>(scratch(c, kS0, (ns ? ns : 1) * sizeof(float)));
+  float* dy = static_cast<float*>(scratch(c, kY0, (ny ? ny : 1) * sizeof(float)));
+  if (!dx || !dh || !ds || !dy) return fail(c, SDR_ENOMEM, "scratch");
+  if (n > 0) SDR_HIP(c, hipMemcpyAsync(dx, x, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if (ntaps > 0) SDR_HIP(c, hipMemcpyAsync(dh, h, ntaps * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if (ns) SDR_HIP(c, hipMemcpyAsync(ds, state, ns * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if ((rc = sdr_resample_f32_dev(c, up, down, dx, n, 1, n, dh, ntaps, ds, ns, dy, ny))) return rc;
+  SDR_HIP(c, hipMemcpyAsync(y, dy, ny * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  if (ns) SDR_HIP(c, hipMemcpyAsync(state, ds, ns * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+int sdr_fm_demod_f32(sdr_ctx* c, const float* I, const float* Q, long long n, float* prev_i, float* prev_q,
+                     float* out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!I || !Q || !prev_i || !prev_q || !out) return fail(c, SDR_EINVAL, "null pointer");
+  if (n <= 0) return fail(c, SDR_EINVAL, "empty block (reference reads I[-1], filter.cpp:100)");
+  float* di = static_cast<float*>(scratch(c, kX0, n * sizeof(float)));
+  float* dq = static_cast<float*>(scratch(c, kX1, n * sizeof(float)));
+  float* dp = static_cast<float*>(scratch(c, kPrev, 4 * sizeof(float)));
+  float* dout = static_cast<float*>(scratch(c, kOut, n * sizeof(float)));
+  if (!di || !dq || !dp || !dout) return fail(c, SDR_ENOMEM, "scratch");
+  SDR_HIP(c, hipMemcpyAsync(di, I, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(dq, Q, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(dp, prev_i, sizeof(float), hipMemcpyHostToDevice, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(dp + 1, prev_q, sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if ((rc = sdr_fm_demod_f32_dev(c, di, dq, n, 1, n, dp, dp + 1, dout, n))) return rc;
+  SDR_HIP(c, hipMemcpyAsync(out, dout, n * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(prev_i, dp, sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(prev_q, dp + 1, sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+static int frontend_host(sdr_ctx* c, sdr::Src src, int D, const float* I, const float* Q, const uint8_t* iq,
+                         long long n, const float* h, int ntaps, float* state_i, float* state_q, int ns,
+                         float* prev_i, float* prev_q, float* demod) {
+  int rc = enter(c);
+  if (rc) return rc;
+  const void* xin = src == sdr::Src::F32 ? (const void*)I : (const void*)iq;
+  if ((rc = check_fir(c, D, n, 1, ntaps, ns, xin, h, state_i))) return rc;
+  if ((src == sdr::Src::F32 && !Q) || !state_q || !prev_i || !prev_q || !demod)
+    return fail(c, SDR_EINVAL, "null pointer");
+  const long long nout = n / D;
+  float* dx0 = nullptr;
+  float* dx1 = nullptr;
+  uint8_t* du = nullptr;
+  if (src == sdr::Src::F32) {
+    dx0 = static_cast<float*>(scratch(c, kX0, n * sizeof(float)));
+    dx1 = static_cast<float*>(scratch(c, kX1, n * sizeof(float)));
+    if (!dx0 || !dx1) return fail(c, SDR_ENOMEM, "scratch");
+  } else {
+    du = static_cast<uint8_t*>(scratch(c, kX0, 2 * n));
+    if (!du) return fail(c, SDR_ENOMEM, "scratch");
+  }
+  float* dh = static_cast<float*>(scratch(c, kH, ntaps * sizeof(float)));
+  float* ds0 = static_cast<float*>(scratch(c, kS0, (ns ? ns : 1) * sizeof(float)));
+  float* ds1 = static_cast<float*>(scratch(c, kS1, (ns ? ns : 1) * sizeof(float)));
+  float* dp = static_cast<float*>(scratch(c, kPrev, 4 * sizeof(float)));
+  float* dout = static_cast<float*>(scratch(c, kOut, nout * sizeof(float)));
+  if (!dh || !ds0 || !ds1 || !dp || !dout) return fail(c, SDR_ENOMEM, "scratch");
+  if (src == sdr::Src::F32) {
+    SDR_HIP(c, hipMemcpyAsync(dx0, I, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    SDR_HIP(c, hipMemcpyAsync(dx1, Q, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  } else {
+    SDR_HIP(c, hipMemcpyAsync(du, iq, 2 * n, hipMemcpyHostToDevice, c->cur));
+  }
+  SDR_HIP(c, hipMemcpyAsync(dh, h, ntaps * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if (ns) {
+    SDR_HIP(c, hipMemcpyAsync(ds0, state_i, ns * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    SDR_HIP(c, hipMemcpyAsync(ds1, state_q, ns * sizeof(float), hipMemcpyHostToDevice, c->cur));
+  }
+  SDR_HIP(c, hipMemcpyAsync(dp, prev_i, sizeof(float), hipMemcpyHostToDevice, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(dp + 1, prev_q, sizeof(float), hipMemcpyHostToDevice, c->cur));
+  if ((rc = frontend_dev(c, src, D, dx0, dx1, du, n, 1, src == sdr::Src::F32 ? n : 2 * n, dh, ntaps, ds0, ds1, ns,
+                         dp, dp + 1, dout, nout)))
+    return rc;
+  SDR_HIP(c, hipMemcpyAsync(demod, dout, nout * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  if (ns) {
+    SDR_HIP(c, hipMemcpyAsync(state_i, ds0, ns * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+    SDR_HIP(c, hipMemcpyAsync(state_q, ds1, ns * sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  }
+  SDR_HIP(c, hipMemcpyAsync(prev_i, dp, sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipMemcpyAsync(prev_q, dp + 1, sizeof(float), hipMemcpyDeviceToHost, c->cur));
+  SDR_HIP(c, hipStreamSynchronize(c->cur));
+  return SDR_OK;
+}
+
+int sdr_frontend_f32(sdr_ctx* c, int D, const float* I, const float* Q, long long n, const float* h, int ntaps,
+                     float* state_i, float* state_q, int ns, float* prev_i, float* prev_q, float* demod) {
+  return frontend_host(c, sdr::Src::F32, D, I, Q, nullptr, n, h, ntaps, state_i, state_q, ns, prev_i, prev_q, demod);
+}
+
+int sdr_frontend_u8(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, const float* h, int ntaps,
+                    float* state_i, float* state_q, int ns, float* prev_i, float* prev_q, float* demod) {
+  return frontend_host(c, sdr::Src::U8, D, nullptr, nullptr, iq, npairs, h, ntaps, state_i, state_q, ns, prev_i,
+                       prev_q, demod);
+}
+
+}  // extern "C"

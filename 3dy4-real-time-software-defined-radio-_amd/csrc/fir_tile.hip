@@ -1,0 +1,518 @@
+// fir_tile.hip -- gfx950 kernels for the reference's FIR / FIR+decimate /
+// fused front end (src/filter.cpp:66-83, 85-102, 123-140, sequenced as in
+// src/project.cpp:86-90).
+//
+// Arithmetic contract (bit-exact with the compiled reference):
+//   y[m] = (...((0 + h[0]*x~[mD]) + h[1]*x~[mD-1]) + ...) + h[T-1]*x~[mD-T+1]
+// with every product and sum rounded separately (no FMA contraction), taps
+// visited in ascending k; x~[p] = x[p] for p >= 0, the saved tail state[ns+p]
+// before the block.  The discriminator keeps the reference's double-precision
+// envelope (std::pow(float,int) promotes, src/filter.cpp:88) and a correctly
+// rounded fp32 divide.
+//
+// Tile kernel structure (fir_tile):
+//   * one 256-thread workgroup = one tile of 256*R consecutive output samples
+//     of one stream; lane l owns outputs R*l .. R*l+R-1 of the tile;
+//   * the tile's input span (D*256*R samples plus a (T-1)-sample halo, i.e.
+//     overlap-save) is staged once into LDS with 16-B coalesced loads; the
+//     halo is re-read from the neighbouring tile's span (L2/MALL), or, for
+//     the first tile of a stream, from the carried `state`;
+//   * every lane then slides down its own D*R-aligned window of the tile in
+//     16-B ds_read_b128 chunks (stride D*R dwords across lanes -- 20 dwords
+//     for D=10, R=2 -- conflict-free) and accumulates all R outputs of both
+//     I and Q channels in registers; tap k is a compile-time index, so the
+//     taps are scalar (SGPR) operands loaded once per wave;
+//   * fused launches apply the discriminator in registers (prev sample via a
+//     wave shuffle / an LDS hand-over between the four waves) and write only
+//     the demodulated stream: decimated I/Q never touch HBM.
+//   * state carry: only the first tile of a stream reads `state`/`prev`, so
+//     that workgroup alone rewrites them after its reads -- no second kernel.
+#include "sdr_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace sdr {
+namespace {
+
+// Tile geometry.  A workgroup computes 4 waves x 64 lanes x R outputs; with
+// the discriminator, lane 0 of every wave re-derives the R outputs just
+// before its wave's span (E = R), so each wave is self-contained (no
+// cross-wave hand-over, no barrier after the fill) at a 1/64 compute cost.
+template <int D, int T, int R, bool DEMOD>
+struct Geom {
+  static_assert((D * R) % 4 == 0, "lane windows must start on 16-B boundaries");
+  static constexpr int E = DEMOD ? R : 0;                          // overlap outputs per wave
+  static constexpr int WADV = 64 * R - E;                          // new outputs per wave
+  static constexpr int ADV = 4 * WADV;                             // new outputs per tile
+  static constexpr int HALO = (T - 1 + 3) / 4 * 4;                 // (T-1) rounded up to a float4
+  static constexpr int SPAN = HALO + D * (R - 1) + 1;              // positions one lane reads
+  static constexpr int NCHUNK = (SPAN + 3) / 4;                    // float4 chunks per lane window
+  static constexpr int SPAN4 = 4 * NCHUNK;                         // tap row length
+  static constexpr int LDS_LEN = D * (3 * WADV + 63 * R) + SPAN4;  // floats per channel
+  static constexpr int LDS4 = LDS_LEN / 4;
+  static constexpr int TAIL = (T + 3) / 4 * 4;                     // prev_* recompute strip
+  // LDS floats: channels, tap rows, two tail strips
+  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4 + 2 * TAIL;
+};
+
+__device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp) {
+  // src/filter.cpp:88-98
+  const float env = (float)((double)I * (double)I + (double)Q * (double)Q);
+  if (env == 0.0f) return 0.0f;
+  const float a = I * (Q - qp);
+  const float b = Q * (I - ip);
+  return (a - b) / env;
+}
+
+// Input sample p (>= 0) of channel c of one stream.
+template <Src SRC>
+__device__ __forceinline__ float in_at(const float* x, const uint8_t* iq, int c, long long p) {
+  if constexpr (SRC == Src::F32) {
+    return x[p];
+  } else {
+    return u8_to_f32(iq[2 * p + c]);
+  }
+}
+
+// Element of the tile span at position p: x~[p], zero outside [-ns, n).
+template <Src SRC>
+__device__ __forceinline__ float edge_at(const float* x, const uint8_t* iq, int c, const float* st, int ns,
+                                         long long n, long long p) {
+  if (p < 0) return p >= -ns ? st[ns + p] : 0.0f;
+  return p < n ? in_at<SRC>(x, iq, c, p) : 0.0f;
+}
+
+template <int D, int T, int R, int NCH, bool DEMOD, Src SRC>
+__global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __restrict__ h) {
+  using G = Geom<D, T, R, DEMOD>;
+  static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
+  static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* lds0 = smem;
+  float* lds1 = smem + G::LDS_LEN;
+  float* htab = smem + 2 * G::LDS_LEN;   // R tap rows
+  float* tail0 = htab + R * G::SPAN4;    // inputs of the block's last output (tile 0)
+  float* tail1 = tail0 + G::TAIL;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int s = blockIdx.x / a.tiles_per_stream;
+  const int t = blockIdx.x - s * a.tiles_per_stream;
+  const long long n = a.n;
+  const long long nout = n / D;
+  const long long m_start = (long long)t * G::ADV - G::E;     // first output computed by the tile
+  const long long pb = (long long)D * m_start - G::HALO;      // stream position of LDS index 0
+  const int ns = a.ns;
+  float* st0 = a.state0 + (long long)s * ns;
+  float* st1 = NCH == 2 ? a.state1 + (long long)s * ns : nullptr;
+  const float* x0 = nullptr;
+  const float* x1 = nullptr;
+  const uint8_t* iq = nullptr;
+  if constexpr (SRC == Src::F32) {
+    x0 = a.x0 + (long long)s * a.x_stride;
+    if (NCH == 2) x1 = a.x1 + (long long)s * a.x_stride;
+  } else {
+    iq = a.iq + (long long)s * a.x_stride;
+  }
+
+  // ---- 1. stage: tap rows, tile span, and (tile 0) everything the state
+  // carry needs.  Every read of the OLD state / prev happens here, before
+  // the only barrier; tile 0 is the only workgroup that reads them and the
+  // only one that rewrites them (step 4), so no second kernel is needed.
+  float old_pi = 0.0f, old_pq = 0.0f;
+  if constexpr (DEMOD) {
+    if (t == 0 && tid == 1) {
+      old_pi = a.prev0[s];
+      old_pq = a.prev1[s];
+    }
+  }
+  // tap rows: htab[r][w] = h[HALO + D*r - w] (0 where that k is not a tap)
+  for (int i = tid; i < R * G::SPAN4; i += kWG) {
+    const int r = i / G::SPAN4, w = i - r * G::SPAN4;
+    const int k = G::HALO + D * r - w;
+    htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
+  }
+  if constexpr (DEMOD) {
+    if (t == 0) {
+      // the T inputs of the block's last decimated sample (prev_* source);
+      // D*(nout-1) - k >= -(T-1) >= -ns, so the old state covers p < 0
+      const long long P = (long long)D * (nout - 1);
+      for (int k = tid; k < T; k += kWG) {
+        const long long p = P - k;
+        tail0[k] = p < 0 ? st0[ns + p] : in_at<SRC>(x0, iq, 0, p);
+        tail1[k] = p < 0 ? st1[ns + p] : in_at<SRC>(x1, iq, 1, p);
+      }
+    }
+  }
+  if (pb >= 0 && pb + G::LDS_LEN <= n) {
+    // interior tile: 16-B (f32) / 8-B (u8) coalesced vector loads, all
+    // issued before the first LDS store
+    constexpr int FULL = G::LDS4 / kWG, REM = G::LDS4 % kWG;
+    float4 v0[FULL + 1], v1[FULL + 1];
+    auto load4 = [&](int i, float4& a0, float4& a1) {
+      const long long p = pb + 4LL * i;
+      if constexpr (SRC == Src::F32) {
+        a0 = *reinterpret_cast<const float4*>(x0 + p);
+        if (NCH == 2) a1 = *reinterpret_cast<const float4*>(x1 + p);
+      } else {
+        const uint2 b = *reinterpret_cast<const uint2*>(iq + 2 * p);
+        a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
+                         u8_to_f32((b.y >> 16) & 0xffu));
+        a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
+                         u8_to_f32(b.y >> 24));
+      }
+    };
+#pragma unroll
+    for (int it = 0; it < FULL; ++it) load4(tid + it * kWG, v0[it], v1[it]);
+    // the ragged last row: clamp the index (a redundant in-bounds load) so
+    // every register is defined and the arrays stay in VGPRs
+    const int il = tid < REM ? tid + FULL * kWG : FULL * kWG - 1;
+    if (REM) load4(il, v0[FULL], v1[FULL]);
+#pragma unroll
+    for (int it = 0; it < FULL; ++it) {
+      const int i = tid + it * kWG;
+      *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[it];
+      if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[it];
+    }
+    if (REM && tid < REM) {
+      *reinterpret_cast<float4*>(lds0 + 4 * il) = v0[FULL];
+      if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * il) = v1[FULL];
+    }
+  } else {
+    // first / last tile of a stream: element-wise, with the state before
+    // the block and zeros past its end (zeros never reach a stored output)
+#pragma unroll 1
+    for (int i = tid; i < G::LDS_LEN; i += kWG) {
+      const long long p = pb + i;
+      lds0[i] = edge_at<SRC>(x0, iq, 0, st0, ns, n, p);
+      if (NCH == 2) lds1[i] = edge_at<SRC>(x1, iq, 1, st1, ns, n, p);
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
+  // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
+  // 4-position chunk c it reads NCH input float4s (its own window; lane
+  // stride D*R dwords, e.g. 20 for D=10: conflict-free ds_read_b128) and R
+  // tap float4s (one address for the whole wave: an LDS broadcast) from
+  // tap rows laid out so that row r, chunk c holds the taps output r applies
+  // to window positions 4c..4c+3.  The next chunk is prefetched; the
+  // sched_barrier keeps the scheduler from hoisting every LDS read of the
+  // unrolled loop (register pressure -> occupancy).
+  const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
+  float acc0[R], acc1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc0[r] = 0.0f;
+    acc1[r] = 0.0f;
+  }
+  {
+    const float* w0 = lds0 + lbase;
+    const float* w1 = lds1 + lbase;
+    constexpr int C0 = G::NCHUNK - 1;
+    float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
+    float4 q1 = q0;
+    if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
+    float4 hq[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) hq[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * C0);
+#pragma unroll
+    for (int c = C0; c >= 0; --c) {
+      float4 n0 = q0, n1 = q1, nh[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) nh[r] = hq[r];
+      if (c > 0) {
+        n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
+        if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+#pragma unroll
+        for (int r = 0; r < R; ++r) nh[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * (c - 1));
+      }
+      const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+      const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        const int w = 4 * c + j;  // window position; output r sits at HALO + D*r
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int k = G::HALO + D * r - w;
+          if (k >= 0 && k < T) {
+            const float hk = j == 0 ? hq[r].x : j == 1 ? hq[r].y : j == 2 ? hq[r].z : hq[r].w;
+            acc0[r] = acc0[r] + hk * e0[j];
+            if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
+          }
+        }
+      }
+      q0 = n0;
+      q1 = n1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) hq[r] = nh[r];
+      // Pin both channels' chains to this chunk: without it LLVM defers
+      // one channel's products past later chunks (holding their operands
+      // live -> 256 VGPRs at R = 4).
+#pragma unroll
+      for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  const long long m0 = m_start + (long long)wave * G::WADV + (long long)R * lane;  // first output of this lane
+  if constexpr (DEMOD) {
+    // ---- 3. discriminator in registers.  The decimated sample before
+    // output r=0 is lane-1's last output (a wave shuffle); lane 0's outputs
+    // are the wave's overlap and are not stored; at the start of the
+    // stream (tile 0, wave 0, lane 1 -> output 0) it is the carried prev_*.
+    float pI = __shfl_up(acc0[R - 1], 1, 64);
+    float pQ = __shfl_up(acc1[R - 1], 1, 64);
+    if (t == 0 && tid == 1) {
+      pI = old_pi;
+      pQ = old_pq;
+    }
+    float d[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float ip = r ? acc0[r - 1] : pI;
+      const float qp = r ? acc1[r - 1] : pQ;
+      d[r] = demod_one(acc0[r], acc1[r], ip, qp);
+    }
+    float* o = a.out + (long long)s * a.out_stride;
+    // vector stores when this stream's row keeps R-float groups aligned
+    // (uniform per workgroup); scalar stores otherwise
+    const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)m_start) % (4u * R)) == 0;
+    if (lane >= 1) {
+      if (vec && m0 + R <= nout) {
+        if constexpr (R == 2) {
+          *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);
+        } else if constexpr (R == 4) {
+          *reinterpret_cast<float4*>(o + m0) = make_float4(d[0], d[1], d[2], d[3]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (m0 + r < nout) o[m0 + r] = d[r];
+      }
+    }
+  } else {
+    float* o = a.y0 + (long long)s * a.y_stride;
+    const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)m_start) % (4u * R)) == 0;
+    if (vec && m0 + R <= nout) {
+      if constexpr (R == 4) {
+        *reinterpret_cast<float4*>(o + m0) = make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
+      } else if constexpr (R == 2) {
+        *reinterpret_cast<float2*>(o + m0) = make_float2(acc0[0], acc0[1]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[m0 + r] = acc0[r];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (m0 + r < nout) o[m0 + r] = acc0[r];
+    }
+  }
+
+  // ---- 4. state carry (tile 0 only; its reads of the old values all
+  // happened before the barrier above)
+  if (t == 0) {
+    if constexpr (DEMOD) {
+      // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
+      // recomputed in the reference's order from the staged strip
+      if (tid == 0) {
+        float yi = 0.0f, yq = 0.0f;
+        for (int k = 0; k < T; ++k) {
+          const float hk = h[k];
+          yi = yi + hk * tail0[k];
+          yq = yq + hk * tail1[k];
+        }
+        a.prev0[s] = yi;
+        a.prev1[s] = yq;
+      }
+    }
+    // state <- last ns input samples (src/filter.cpp:139)
+    for (int j = tid; j < ns; j += kWG) {
+      const long long p = n - ns + j;
+      st0[j] = in_at<SRC>(x0, iq, 0, p);
+      if (NCH == 2) st1[j] = in_at<SRC>(x1, iq, 1, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------- generic path --
+// Any D / T / ns the tiled kernel is not instantiated for.  One thread per
+// output sample, same operation order; x~ read straight from global memory.
+template <Src SRC>
+__global__ __launch_bounds__(kWG) void fir_generic(FirLaunch a, const float* __restrict__ h, int nch,
+                                                   float* y0, float* y1, long long y_stride) {
+  const int s = blockIdx.y;
+  const long long m = (long long)blockIdx.x * kWG + threadIdx.x;
+  const long long nout = a.n / a.D;
+  if (m >= nout) return;
+  const float* x0 = SRC == Src::F32 ? a.x0 + (long long)s * a.x_stride : nullptr;
+  const float* x1 = SRC == Src::F32 && nch == 2 ? a.x1 + (long long)s * a.x_stride : nullptr;
+  const uint8_t* iq = SRC == Src::U8 ? a.iq + (long long)s * a.x_stride : nullptr;
+  const float* st0 = a.state0 + (long long)s * a.ns;
+  const float* st1 = nch == 2 ? a.state1 + (long long)s * a.ns : nullptr;
+  const long long P = (long long)a.D * m;
+  float acc0 = 0.0f, acc1 = 0.0f;
+  for (int k = 0; k < a.ntaps; ++k) {
+    const long long p = P - k;
+    const float hk = h[k];
+    const float v0 = p >= 0 ? in_at<SRC>(x0, iq, 0, p) : st0[a.ns + p];
+    acc0 = acc0 + hk * v0;
+    if (nch == 2) {
+      const float v1 = p >= 0 ? in_at<SRC>(x1, iq, 1, p) : st1[a.ns + p];
+      acc1 = acc1 + hk * v1;
+    }
+  }
+  y0[(long long)s * y_stride + m] = acc0;
+  if (nch == 2) y1[(long long)s * y_stride + m] = acc1;
+}
+
+// state <- last ns inputs; a separate launch after fir_generic (whose
+// threads may still be reading the old state otherwise).
+template <Src SRC>
+__global__ __launch_bounds__(kWG) void commit_state(FirLaunch a, int nch) {
+  const int s = blockIdx.y;
+  const int j = blockIdx.x * kWG + threadIdx.x;
+  if (j >= a.ns) return;
+  const float* x0 = SRC == Src::F32 ? a.x0 + (long long)s * a.x_stride : nullptr;
+  const float* x1 = SRC == Src::F32 && nch == 2 ? a.x1 + (long long)s * a.x_stride : nullptr;
+  const uint8_t* iq = SRC == Src::U8 ? a.iq + (long long)s * a.x_stride : nullptr;
+  const long long p = a.n - a.ns + j;
+  a.state0[(long long)s * a.ns + j] = in_at<SRC>(x0, iq, 0, p);
+  if (nch == 2) a.state1[(long long)s * a.ns + j] = in_at<SRC>(x1, iq, 1, p);
+}
+
+// fmDemodArctan over nstreams x n decimated samples (src/filter.cpp:85-102).
+// Thread 0 of a stream is the only reader of prev_* and rewrites them.
+__global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float* Q, long long n, long long stride,
+                                                    float* prev_i, float* prev_q, float* out, long long out_stride) {
+  const int s = blockIdx.y;
+  const long long k = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (k >= n) return;
+  const float* Is = I + (long long)s * stride;
+  const float* Qs = Q + (long long)s * stride;
+  float ip, qp;
+  if (k == 0) {
+    ip = prev_i[s];
+    qp = prev_q[s];
+  } else {
+    ip = Is[k - 1];
+    qp = Qs[k - 1];
+  }
+  out[(long long)s * out_stride + k] = demod_one(Is[k], Qs[k], ip, qp);
+  if (k == 0) {
+    prev_i[s] = Is[n - 1];
+    prev_q[s] = Qs[n - 1];
+  }
+}
+
+// ------------------------------------------------------------ dispatch ----
+template <int D, int T, int R, int NCH, bool DEMOD, Src SRC>
+hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
+  using G = Geom<D, T, R, DEMOD>;
+  FirLaunch a = a0;
+  const long long nout = a.n / D;
+  a.tiles_per_stream = (int)((nout + G::ADV - 1) / G::ADV);
+  const size_t lds = (size_t)G::SMEM * sizeof(float);
+  const long long blocks = (long long)a.tiles_per_stream * a.nstreams;
+  if (blocks <= 0 || blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((fir_tile<D, T, R, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(kWG), lds, st, a, h);
+  return hipGetLastError();
+}
+
+// Fast-path table.  R is chosen so that D*R is a multiple of 4 (aligned lane
+// windows) and the LDS footprint allows >= 2 workgroups per CU.
+template <int NCH, bool DEMOD, Src SRC>
+hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, bool* handled) {
+  *handled = true;
+  if (a.ntaps == 101) {
+    switch (a.D) {
+      case 10: return run_tile<10, 101, 2, NCH, DEMOD, SRC>(a, h, st);
+      case 5: return run_tile<5, 101, 4, NCH, DEMOD, SRC>(a, h, st);
+      case 1:
+        if constexpr (!DEMOD) return run_tile<1, 101, 4, NCH, DEMOD, SRC>(a, h, st);
+        break;
+      default: break;
+    }
+  }
+  *handled = false;
+  return hipSuccess;
+}
+
+// Only tile 0 may touch the carried state: tile 1's span must start at p >= 0.
+template <int D, int T, int R, bool DEMOD>
+constexpr bool tile_ok(int ns) {
+  using G = Geom<D, T, R, DEMOD>;
+  return ns >= T - 1 && (long long)D * (G::ADV - G::E) - G::HALO >= 0;
+}
+
+}  // namespace
+
+bool fir_has_fast_path(int D, int ntaps, int ns, int nch, bool demod, Src src) {
+  if (ntaps != 101 || ns < ntaps - 1) return false;
+  if (src == Src::U8 && nch != 2) return false;
+  if (demod && nch != 2) return false;
+  switch (D) {
+    case 10: return demod ? tile_ok<10, 101, 2, true>(ns) : tile_ok<10, 101, 2, false>(ns);
+    case 5: return demod ? tile_ok<5, 101, 4, true>(ns) : tile_ok<5, 101, 4, false>(ns);
+    case 1: return !demod && tile_ok<1, 101, 4, false>(ns);
+    default: return false;
+  }
+}
+
+hipError_t launch_demod(const float* I, const float* Q, long long n, int nstreams, long long stride, float* prev_i,
+                        float* prev_q, float* out, long long out_stride, hipStream_t st) {
+  const long long gx = (n + kWG - 1) / kWG;
+  hipLaunchKernelGGL(demod_kernel, dim3((unsigned)gx, (unsigned)nstreams), dim3(kWG), 0, st, I, Q, n, stride, prev_i,
+                     prev_q, out, out_stride);
+  return hipGetLastError();
+}
+
+// a.y0/a.y1 receive FIR outputs (non-demod); scratch_y{0,1} ([nstreams][n/D])
+// hold decimated I/Q when a demod launch takes the generic path.
+hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, Src src, hipStream_t st,
+                      float* scratch_y0, float* scratch_y1, bool allow_fast) {
+  if (allow_fast && fir_has_fast_path(a.D, a.ntaps, a.ns, nch, demod, src)) {
+    bool handled = false;
+    hipError_t e = hipSuccess;
+    if (src == Src::U8) {
+      e = dispatch_tile<2, true, Src::U8>(a, h, st, &handled);
+    } else if (demod) {
+      e = dispatch_tile<2, true, Src::F32>(a, h, st, &handled);
+    } else if (nch == 1) {
+      e = dispatch_tile<1, false, Src::F32>(a, h, st, &handled);
+    } else {
+      e = dispatch_tile<2, false, Src::F32>(a, h, st, &handled);
+    }
+    if (handled) return e;
+  }
+  // generic: FIR (+ separate state commit) (+ separate demod)
+  const long long nout = a.n / a.D;
+  float* y0 = demod ? scratch_y0 : a.y0;
+  float* y1 = demod ? scratch_y1 : a.y1;
+  const long long ys = demod ? nout : a.y_stride;
+  const dim3 grid((unsigned)((nout + kWG - 1) / kWG), (unsigned)a.nstreams);
+  if (src == Src::U8)
+    hipLaunchKernelGGL(fir_generic<Src::U8>, grid, dim3(kWG), 0, st, a, h, nch, y0, y1, ys);
+  else
+    hipLaunchKernelGGL(fir_generic<Src::F32>, grid, dim3(kWG), 0, st, a, h, nch, y0, y1, ys);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const dim3 cgrid((unsigned)((a.ns + kWG - 1) / kWG), (unsigned)a.nstreams);
+  if (a.ns > 0) {
+    if (src == Src::U8)
+      hipLaunchKernelGGL(commit_state<Src::U8>, cgrid, dim3(kWG), 0, st, a, nch);
+    else
+      hipLaunchKernelGGL(commit_state<Src::F32>, cgrid, dim3(kWG), 0, st, a, nch);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (demod) return launch_demod(y0, y1, nout, a.nstreams, nout, a.prev0, a.prev1, a.out, a.out_stride, st);
+  return hipSuccess;
+}
+
+}  // namespace sdr

@@ -1,0 +1,72 @@
+// sdr_common.hpp -- shared launch descriptors and helpers for the gfx950
+// RF front-end kernels.  Internal to libsdrhip.so (the public surface is
+// include/sdr_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sdr {
+
+// Every FIR-family kernel runs 256-thread workgroups: four wave64s, one per
+// SIMD of a CU.
+constexpr int kWG = 256;
+
+enum class Src : int { F32 = 0, U8 = 1 };
+
+// One launch = the next block of `nstreams` independent streams.  Stream s:
+//   input   x{0,1} + s*x_stride (f32 planar I/Q), or iq + s*x_stride bytes (u8)
+//   state   state{0,1} + s*ns          (the reference's `state` vectors)
+//   prev    prev{0,1}[s]               (fmDemodArctan's prev_I / prev_Q)
+//   output  y0 + s*y_stride            (FIR-only launches)
+//           out + s*out_stride         (demodulated, fused launches)
+struct FirLaunch {
+  const float* x0;
+  const float* x1;
+  const uint8_t* iq;
+  long long x_stride;
+  long long n;  // input samples (IQ pairs for the fused path) per stream
+  int nstreams;
+  int ntaps;
+  int D;
+  float* state0;
+  float* state1;
+  int ns;
+  float* prev0;
+  float* prev1;
+  float* y0;
+  float* y1;
+  long long y_stride;
+  float* out;
+  long long out_stride;
+  int tiles_per_stream;
+};
+
+// Exact reference conversion of one wire byte, src/iofunc.cpp:118:
+// float(((unsigned char)u - 128) / 128.0).  (u-128)/128 is a multiple of
+// 2^-7 with |value| <= 1, so the float product below is the same number.
+__device__ __forceinline__ float u8_to_f32(uint32_t u) { return (float)((int)u - 128) * 0.0078125f; }
+
+// Host-side launchers, one per kernel family (defined next to the kernels).
+// allow_fast = false forces the generic kernel (misaligned buffers).
+hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, Src src, hipStream_t st,
+                      float* scratch_y0, float* scratch_y1, bool allow_fast);
+hipError_t launch_demod(const float* I, const float* Q, long long n, int nstreams, long long stride,
+                        float* prev_i, float* prev_q, float* out, long long out_stride, hipStream_t st);
+hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
+                           const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
+                           long long ny, float* scratch_taps, hipStream_t st);
+hipError_t launch_synth_fm_u8(uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
+                              unsigned long long seed, hipStream_t st);
+hipError_t launch_u8_to_planar(const uint8_t* iq, long long npairs, int nstreams, long long iq_stride, float* I,
+                               float* Q, long long x_stride, hipStream_t st);
+
+// Whether the tiled fast path handles (D, ntaps, ns) for this source; false
+// means launch_fir takes the generic path (still exact, slower).
+bool fir_has_fast_path(int D, int ntaps, int ns, int nch, bool demod, Src src);
+
+// Bytes of scratch the resampler needs for its polyphase tap table.
+size_t resample_scratch_floats(int up, int ntaps);
+
+}  // namespace sdr

@@ -1,0 +1,348 @@
+"""Python binding of libsdrhip.so (the C ABI in include/sdr_hip.h).
+
+This is the host-side face of the MI355X RF front end for tests, the
+benchmark and Python callers; C/C++ callers use the C ABI or the drop-in
+filter.h implementation (host/filter_hip.cpp) directly.
+
+Two layers, mirroring the C ABI:
+
+* ``Context`` host-array methods (``fir_decim``, ``fir_block``,
+  ``resample``, ``fm_demod``, ``frontend``, ``frontend_u8``) -- numpy in,
+  numpy out, one block of one stream, state arrays updated in place: the
+  reference's filter.h contract (src/filter.cpp).
+* ``Context`` ``*_dev`` methods -- device-resident and batched: arguments are
+  device pointers (ints) or objects exposing ``data_ptr()`` (torch tensors
+  on the GPU).  They enqueue on the context's stream and return at once.
+
+There is no CPU fallback anywhere: if the shared library is missing or no
+GPU is present, constructing a Context raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libsdrhip.so")
+DROPIN_PATH = os.path.join(PKG_DIR, "libdy4filter_hip.so")
+REPO_DIR = os.path.dirname(PKG_DIR)
+HEADER_PATH = os.path.join(REPO_DIR, "include", "sdr_hip.h")
+
+SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_ENODEV = 0, -1, -2, -3, -4
+
+_lib = None
+
+_vp = C.c_void_p
+_fp = C.POINTER(C.c_float)
+_ll = C.c_longlong
+_i = C.c_int
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS = {
+    "sdr_version": [],
+    "sdr_strerror": [_i],
+    "sdr_device_count": [C.POINTER(_i)],
+    "sdr_ctx_create": [_i, C.POINTER(_vp)],
+    "sdr_ctx_destroy": [_vp],
+    "sdr_ctx_set_stream": [_vp, _vp],
+    "sdr_ctx_get_stream": [_vp],
+    "sdr_ctx_synchronize": [_vp],
+    "sdr_ctx_last_error": [_vp],
+    "sdr_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
+    "sdr_dev_free": [_vp, _vp],
+    "sdr_copy_h2d": [_vp, _vp, _vp, C.c_size_t],
+    "sdr_copy_d2h": [_vp, _vp, _vp, C.c_size_t],
+    "sdr_dev_memset": [_vp, _vp, _i, C.c_size_t],
+    "sdr_resample_out_len": [_i, _i, _ll],
+    "sdr_taps_lpf": [C.c_float, C.c_float, _i, _i, _vp],
+    "sdr_taps_bpf": [C.c_float, C.c_float, C.c_float, _i, _i, _vp],
+    "sdr_fir_block_f32": [_vp, _vp, _ll, _vp, _i, _vp, _i, _vp],
+    "sdr_fir_decim_f32": [_vp, _i, _vp, _ll, _vp, _i, _vp, _i, _vp],
+    "sdr_resample_f32": [_vp, _i, _i, _vp, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_fm_demod_f32": [_vp, _vp, _vp, _ll, _vp, _vp, _vp],
+    "sdr_frontend_f32": [_vp, _i, _vp, _vp, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp],
+    "sdr_frontend_u8": [_vp, _i, _vp, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp],
+    "sdr_fir_decim_f32_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_fir_block_f32_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_fm_demod_f32_dev": [_vp, _vp, _vp, _ll, _i, _ll, _vp, _vp, _vp, _ll],
+    "sdr_frontend_f32_dev": [_vp, _i, _vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _ll],
+    "sdr_frontend_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _ll],
+    "sdr_resample_f32_dev": [_vp, _i, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
+    "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
+}
+_RESTYPE = {"sdr_version": C.c_char_p, "sdr_strerror": C.c_char_p, "sdr_ctx_last_error": C.c_char_p,
+            "sdr_ctx_get_stream": _vp, "sdr_resample_out_len": _ll}
+
+EXPORTED = tuple(_SIGS)
+
+
+class SdrError(RuntimeError):
+    def __init__(self, code: int, where: str, detail: str = ""):
+        self.code = code
+        super().__init__(f"{where}: {lib().sdr_strerror(code).decode()} ({detail})")
+
+
+def lib() -> C.CDLL:
+    """Load libsdrhip.so (raises if it was not built -- no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: build it (python -c 'import __graft_entry__ as g; g.build()')")
+        L = C.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = _RESTYPE.get(name, _i)
+        _lib = L
+    return _lib
+
+
+def version() -> str:
+    return lib().sdr_version().decode()
+
+
+def device_count() -> int:
+    n = _i(0)
+    lib().sdr_device_count(C.byref(n))
+    return n.value
+
+
+def resample_out_len(up: int, down: int, n: int) -> int:
+    """(size_t)((n / (float)down) * up) -- src/filter.cpp:149."""
+    return int(lib().sdr_resample_out_len(up, down, n))
+
+
+def taps_lpf(Fs: float, Fc: float, ntaps: int, up: int = 1) -> np.ndarray:
+    """impulseResponseLPF (src/filter.cpp:14-29), bit-identical."""
+    h = np.empty(ntaps, np.float32)
+    if lib().sdr_taps_lpf(Fs, Fc, ntaps, up, h.ctypes.data) != SDR_OK:
+        raise ValueError("bad tap design arguments")
+    return h
+
+
+def taps_bpf(Fs: float, Fb: float, Fe: float, ntaps: int, up: int = 1) -> np.ndarray:
+    """impulseResponseBPF (src/filter.cpp:31-49), bit-identical."""
+    h = np.empty(ntaps, np.float32)
+    if lib().sdr_taps_bpf(Fs, Fb, Fe, ntaps, up, h.ctypes.data) != SDR_OK:
+        raise ValueError("bad tap design arguments")
+    return h
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    if isinstance(x, np.ndarray):
+        return int(x.ctypes.data)
+    raise TypeError(f"cannot take a device pointer of {type(x)!r}")
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _inplace(a, what):
+    if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous and a.flags.writeable):
+        raise TypeError(f"{what} must be a writeable contiguous float32 numpy array (updated in place)")
+    return a
+
+
+class Context:
+    """One GPU + one HIP stream + scratch buffers (sdr_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self._c = _vp()
+        rc = lib().sdr_ctx_create(device, C.byref(self._c))
+        if rc != SDR_OK:
+            raise SdrError(rc, f"sdr_ctx_create({device})")
+        self.device = device
+
+    # -- lifetime / stream
+    def close(self):
+        if self._c:
+            lib().sdr_ctx_destroy(self._c)
+            self._c = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, hip_stream: int | None):
+        """Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
+        self._check(lib().sdr_ctx_set_stream(self._c, hip_stream or None), "set_stream")
+
+    @property
+    def stream(self) -> int:
+        return lib().sdr_ctx_get_stream(self._c) or 0
+
+    def synchronize(self):
+        self._check(lib().sdr_ctx_synchronize(self._c), "synchronize")
+
+    def last_error(self) -> str:
+        return lib().sdr_ctx_last_error(self._c).decode()
+
+    def _check(self, rc: int, where: str):
+        if rc != SDR_OK:
+            raise SdrError(rc, where, self.last_error())
+
+    # -- host arrays, one block (filter.h contract) ----------------------
+    def fir_block(self, x, h, state):
+        """blockConvolveFIR (src/filter.cpp:66-83)."""
+        x, h, state = _f32(x), _f32(h), _inplace(state, "state")
+        y = np.empty(len(x), np.float32)
+        self._check(lib().sdr_fir_block_f32(self._c, _ptr(x), len(x), _ptr(h), len(h), _ptr(state), len(state),
+                                            _ptr(y)), "fir_block")
+        return y
+
+    def fir_decim(self, D, x, h, state):
+        """downsampleBlockConvolveFIR (src/filter.cpp:123-140)."""
+        x, h, state = _f32(x), _f32(h), _inplace(state, "state")
+        y = np.empty(max(len(x) // max(D, 1), 1), np.float32)
+        self._check(lib().sdr_fir_decim_f32(self._c, D, _ptr(x), len(x), _ptr(h), len(h), _ptr(state),
+                                            len(state), _ptr(y)), "fir_decim")
+        return y[:len(x) // D]
+
+    def resample(self, up, down, x, h, state):
+        """resampleBlockConvolveFIR (src/filter.cpp:142-173)."""
+        x, h, state = _f32(x), _f32(h), _inplace(state, "state")
+        ny = resample_out_len(up, down, len(x))
+        y = np.empty(max(ny, 1), np.float32)
+        self._check(lib().sdr_resample_f32(self._c, up, down, _ptr(x), len(x), _ptr(h), len(h), _ptr(state),
+                                           len(state), _ptr(y), max(ny, 0)), "resample")
+        return y[:ny]
+
+    def fm_demod(self, I, Q, prev):
+        """fmDemodArctan (src/filter.cpp:85-102); prev = float32[2] {prev_I, prev_Q}, in place."""
+        I, Q, prev = _f32(I), _f32(Q), _inplace(prev, "prev")
+        out = np.empty(max(len(I), 1), np.float32)
+        pv = prev.ctypes.data
+        self._check(lib().sdr_fm_demod_f32(self._c, _ptr(I), _ptr(Q), len(I), pv, pv + 4, _ptr(out)), "fm_demod")
+        return out[:len(I)]
+
+    def frontend(self, D, I, Q, h, state_i, state_q, prev):
+        """Fused src/project.cpp:86-90 in one launch; returns the demodulated block."""
+        I, Q, h = _f32(I), _f32(Q), _f32(h)
+        _inplace(state_i, "state_i"), _inplace(state_q, "state_q"), _inplace(prev, "prev")
+        out = np.empty(max(len(I) // max(D, 1), 1), np.float32)
+        pv = prev.ctypes.data
+        self._check(lib().sdr_frontend_f32(self._c, D, _ptr(I), _ptr(Q), len(I), _ptr(h), len(h), _ptr(state_i),
+                                           _ptr(state_q), len(state_i), pv, pv + 4, _ptr(out)), "frontend")
+        return out[:len(I) // D]
+
+    def frontend_u8(self, D, iq, h, state_i, state_q, prev):
+        """Fused front end straight from interleaved u8 IQ (src/iofunc.cpp:117-119 folded in)."""
+        iq = np.ascontiguousarray(iq, dtype=np.uint8)
+        h = _f32(h)
+        _inplace(state_i, "state_i"), _inplace(state_q, "state_q"), _inplace(prev, "prev")
+        npairs = len(iq) // 2
+        out = np.empty(max(npairs // max(D, 1), 1), np.float32)
+        pv = prev.ctypes.data
+        self._check(lib().sdr_frontend_u8(self._c, D, _ptr(iq), npairs, _ptr(h), len(h), _ptr(state_i),
+                                          _ptr(state_q), len(state_i), pv, pv + 4, _ptr(out)), "frontend_u8")
+        return out[:npairs // D]
+
+    # -- device pointers, batched ------------------------------------------
+    def fir_decim_dev(self, D, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
+        self._check(lib().sdr_fir_decim_f32_dev(self._c, D, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
+                                                _ptr(state), ns, _ptr(y), y_stride), "fir_decim_dev")
+
+    def fir_block_dev(self, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
+        self._check(lib().sdr_fir_block_f32_dev(self._c, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
+                                                _ptr(state), ns, _ptr(y), y_stride), "fir_block_dev")
+
+    def fm_demod_dev(self, I, Q, n, nstreams, stride, prev_i, prev_q, out, out_stride):
+        self._check(lib().sdr_fm_demod_f32_dev(self._c, _ptr(I), _ptr(Q), n, nstreams, stride, _ptr(prev_i),
+                                               _ptr(prev_q), _ptr(out), out_stride), "fm_demod_dev")
+
+    def frontend_dev(self, D, I, Q, n, nstreams, x_stride, h, ntaps, state_i, state_q, ns, prev_i, prev_q, out,
+                     out_stride):
+        self._check(lib().sdr_frontend_f32_dev(self._c, D, _ptr(I), _ptr(Q), n, nstreams, x_stride, _ptr(h), ntaps,
+                                               _ptr(state_i), _ptr(state_q), ns, _ptr(prev_i), _ptr(prev_q),
+                                               _ptr(out), out_stride), "frontend_dev")
+
+    def frontend_u8_dev(self, D, iq, npairs, nstreams, iq_stride, h, ntaps, state_i, state_q, ns, prev_i, prev_q,
+                        out, out_stride):
+        self._check(lib().sdr_frontend_u8_dev(self._c, D, _ptr(iq), npairs, nstreams, iq_stride, _ptr(h), ntaps,
+                                              _ptr(state_i), _ptr(state_q), ns, _ptr(prev_i), _ptr(prev_q),
+                                              _ptr(out), out_stride), "frontend_u8_dev")
+
+    def resample_dev(self, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
+        self._check(lib().sdr_resample_f32_dev(self._c, up, down, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
+                                               _ptr(state), ns, _ptr(y), y_stride), "resample_dev")
+
+    def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
+        self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")
+
+    def u8_to_planar_dev(self, iq, npairs, nstreams, iq_stride, I, Q, x_stride):
+        self._check(lib().sdr_u8_to_planar_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, _ptr(I), _ptr(Q),
+                                               x_stride), "u8_to_planar_dev")
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Function names declared in include/sdr_hip.h."""
+    import re
+
+    text = open(path).read()
+    return sorted(set(re.findall(r"\b(sdr_[a-z0-9_]+)\s*\(", text)))
+
+
+class DeviceArray:
+    """A device buffer owned through the C ABI (no torch needed)."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = _vp()
+        ctx._check(lib().sdr_dev_alloc(ctx._c, max(self.nbytes, 16), C.byref(p)), "dev_alloc")
+        self.ptr = int(p.value)
+
+    @classmethod
+    def from_numpy(cls, ctx: Context, a: np.ndarray) -> "DeviceArray":
+        a = np.ascontiguousarray(a)
+        d = cls(ctx, a.nbytes)
+        d.upload(a)
+        return d
+
+    def upload(self, a: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        self.ctx._check(lib().sdr_copy_h2d(self.ctx._c, self.ptr + offset, a.ctypes.data, a.nbytes), "copy_h2d")
+
+    def download(self, dtype=np.float32, count: int | None = None, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if count is None:
+            count = (self.nbytes - offset) // dt.itemsize
+        out = np.empty(count, dt)
+        self.ctx._check(lib().sdr_copy_d2h(self.ctx._c, out.ctypes.data, self.ptr + offset, out.nbytes), "copy_d2h")
+        return out
+
+    def fill(self, byte: int = 0):
+        self.ctx._check(lib().sdr_dev_memset(self.ctx._c, self.ptr, byte, self.nbytes), "memset")
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+    def free(self):
+        if self.ptr:
+            lib().sdr_dev_free(self.ctx._c, self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

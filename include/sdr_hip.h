@@ -1,0 +1,150 @@
+/*
+ * sdr_hip.h -- C ABI of the MI355X (gfx950) RF front-end library (libsdrhip.so).
+ *
+ * This is the drop-in boundary for the hot path of the reference's DSP block
+ * library, src/filter.cpp, whose C++ interface is include/filter.h:17-34
+ * (ghotrs4/3DY4-Real-Time-Software-defined-Radio-).  Plain pointers and sizes
+ * only: no torch, no HIP types in any signature (streams travel as void*).
+ *
+ * Two families of entry points:
+ *
+ *  1. Host-pointer, synchronous calls (``sdr_*_f32``): one block of one
+ *     stream, exactly the contract of the filter.h function each one
+ *     replaces -- outputs valid on return, in/out state arrays updated in
+ *     place.  The drop-in filter implementation (host/filter_hip.cpp) is
+ *     built on these.  They copy over PCIe; they exist for compatibility and
+ *     parity, not for throughput.
+ *
+ *  2. Device-resident, batched, stream-ordered calls (``*_dev``): nstreams
+ *     independent streams in one launch, every pointer is device memory, the
+ *     call only enqueues work on the context's HIP stream.  Stream s reads
+ *     its n input samples at  x + s*x_stride  and owns row s of each state
+ *     array ([nstreams][ns], row stride ns) and element s of each prev array.
+ *     One call == the next block of every stream: state carries exactly as
+ *     the reference carries it between calls.  These are what bench.py times.
+ *
+ * Arithmetic contract: every kernel reproduces the reference's fp32 operation
+ * order (taps summed k = 0..T-1 from 0.0f with separately rounded multiply
+ * and add, discriminator envelope summed in double) so results are
+ * bit-identical to the compiled reference; see DESIGN.md "Parity".
+ *
+ * Errors: every call returns SDR_OK (0) or a negative code.  SDR_EINVAL marks
+ * an argument combination for which the reference itself would read or write
+ * out of bounds (e.g. n % D != 0 in downsampleBlockConvolveFIR,
+ * src/filter.cpp:127-132); sdr_ctx_last_error() says which.
+ *
+ * Threading: a context (one device + one HIP stream + scratch buffers) must
+ * not be used by two threads at once; use one context per thread (the drop-in
+ * keeps a thread_local one, matching src/project.cpp:299-302's two threads).
+ */
+#ifndef SDR_HIP_H
+#define SDR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDR_OK 0
+#define SDR_EINVAL (-1) /* precondition the reference leaves as UB / bad argument */
+#define SDR_EHIP (-2)   /* HIP runtime / launch failure */
+#define SDR_ENOMEM (-3) /* device allocation failed */
+#define SDR_ENODEV (-4) /* no such device */
+
+typedef struct sdr_ctx sdr_ctx;
+
+/* ------------------------------------------------------------ context -- */
+const char *sdr_version(void);
+const char *sdr_strerror(int code);
+int sdr_device_count(int *count);
+int sdr_ctx_create(int device, sdr_ctx **ctx);
+int sdr_ctx_destroy(sdr_ctx *ctx);
+/* Use an external HIP stream (hipStream_t as void*); NULL restores the
+ * context's own stream. */
+int sdr_ctx_set_stream(sdr_ctx *ctx, void *hip_stream);
+void *sdr_ctx_get_stream(sdr_ctx *ctx);
+int sdr_ctx_synchronize(sdr_ctx *ctx);
+const char *sdr_ctx_last_error(sdr_ctx *ctx);
+
+/* Device memory helpers so a C/C++ caller needs no HIP headers. */
+int sdr_dev_alloc(sdr_ctx *ctx, size_t bytes, void **ptr);
+int sdr_dev_free(sdr_ctx *ctx, void *ptr);
+int sdr_copy_h2d(sdr_ctx *ctx, void *dst, const void *src, size_t bytes); /* synchronous */
+int sdr_copy_d2h(sdr_ctx *ctx, void *dst, const void *src, size_t bytes); /* synchronous */
+int sdr_dev_memset(sdr_ctx *ctx, void *dst, int value, size_t bytes);   /* stream-ordered */
+
+/* --------------------------------------------------- coefficient design -- */
+/* impulseResponseLPF / impulseResponseBPF, src/filter.cpp:14-49
+ * (filter.h:17, :27): windowed-sinc taps with the up-factor gain folded in,
+ * bit-identical to the reference.  Host code (one-time setup). h: ntaps. */
+int sdr_taps_lpf(float Fs, float Fc, int ntaps, int up, float *h);
+int sdr_taps_bpf(float Fs, float Fb, float Fe, int ntaps, int up, float *h);
+
+/* ------------------------------------------------------------- sizing -- */
+/* Output length of resampleBlockConvolveFIR, src/filter.cpp:149:
+ * (size_t)((n / (float)down) * up). */
+long long sdr_resample_out_len(int up, int down, long long n);
+
+/* -------------------------------------------- host-pointer, synchronous -- */
+/* blockConvolveFIR, src/filter.cpp:66-83 (filter.h:19).  y: n floats. */
+int sdr_fir_block_f32(sdr_ctx *ctx, const float *x, long long n, const float *h, int ntaps,
+                      float *state, int ns, float *y);
+/* downsampleBlockConvolveFIR, src/filter.cpp:123-140 (filter.h:25).
+ * y: n/D floats; requires n % D == 0. */
+int sdr_fir_decim_f32(sdr_ctx *ctx, int D, const float *x, long long n, const float *h, int ntaps,
+                      float *state, int ns, float *y);
+/* resampleBlockConvolveFIR, src/filter.cpp:142-173 (filter.h:26).
+ * y: sdr_resample_out_len(up, down, n) floats (y_cap is checked against it). */
+int sdr_resample_f32(sdr_ctx *ctx, int up, int down, const float *x, long long n, const float *h,
+                     int ntaps, float *state, int ns, float *y, long long y_cap);
+/* fmDemodArctan, src/filter.cpp:85-102 (filter.h:20).  out: n floats. */
+int sdr_fm_demod_f32(sdr_ctx *ctx, const float *I, const float *Q, long long n, float *prev_i,
+                     float *prev_q, float *out);
+/* The whole front end of src/project.cpp:86-90 fused into one launch:
+ * FIR+decimate(I), FIR+decimate(Q), discriminator.  demod: n/D floats. */
+int sdr_frontend_f32(sdr_ctx *ctx, int D, const float *I, const float *Q, long long n, const float *h,
+                     int ntaps, float *state_i, float *state_q, int ns, float *prev_i, float *prev_q,
+                     float *demod);
+/* Same, reading the RTL-SDR wire format directly: interleaved u8 I/Q
+ * (2*npairs bytes) converted as src/iofunc.cpp:117-119 and de-interleaved as
+ * src/project.cpp:78-81, inside the kernel. */
+int sdr_frontend_u8(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs, const float *h, int ntaps,
+                    float *state_i, float *state_q, int ns, float *prev_i, float *prev_q, float *demod);
+
+/* -------------------------------- device-resident, batched, stream-ordered -- */
+/* Pointers 16-byte aligned and strides multiples of 4 elements (the kernels
+ * stream 16-B vectors); otherwise SDR_EINVAL. */
+int sdr_fir_decim_f32_dev(sdr_ctx *ctx, int D, const float *x, long long n, int nstreams, long long x_stride,
+                          const float *h, int ntaps, float *state, int ns, float *y, long long y_stride);
+int sdr_fir_block_f32_dev(sdr_ctx *ctx, const float *x, long long n, int nstreams, long long x_stride,
+                          const float *h, int ntaps, float *state, int ns, float *y, long long y_stride);
+int sdr_fm_demod_f32_dev(sdr_ctx *ctx, const float *I, const float *Q, long long n, int nstreams,
+                         long long stride, float *prev_i, float *prev_q, float *out, long long out_stride);
+int sdr_frontend_f32_dev(sdr_ctx *ctx, int D, const float *I, const float *Q, long long n, int nstreams,
+                         long long x_stride, const float *h, int ntaps, float *state_i, float *state_q, int ns,
+                         float *prev_i, float *prev_q, float *demod, long long out_stride);
+/* iq_stride in bytes (multiple of 8); npairs per stream. */
+int sdr_frontend_u8_dev(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs, int nstreams,
+                        long long iq_stride, const float *h, int ntaps, float *state_i, float *state_q, int ns,
+                        float *prev_i, float *prev_q, float *demod, long long out_stride);
+int sdr_resample_f32_dev(sdr_ctx *ctx, int up, int down, const float *x, long long n, int nstreams,
+                         long long x_stride, const float *h, int ntaps, float *state, int ns, float *y,
+                         long long y_stride);
+
+/* ---------------------------------------------------- synthetic input -- */
+/* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the
+ * device (counter-based, keyed by (seed, stream, sample)); used by the
+ * benchmark so no host traffic is needed.  Not bit-identical to the numpy
+ * generator in sdrhip/synth.py -- both are just "FM-like" test signals. */
+int sdr_synth_fm_u8_dev(sdr_ctx *ctx, uint8_t *iq, long long npairs, int nstreams, long long iq_stride,
+                        unsigned long long seed);
+/* u8 interleaved -> planar f32 (src/iofunc.cpp:117-119 + project.cpp:78-81). */
+int sdr_u8_to_planar_dev(sdr_ctx *ctx, const uint8_t *iq, long long npairs, int nstreams, long long iq_stride,
+                         float *I, float *Q, long long x_stride);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDR_HIP_H */

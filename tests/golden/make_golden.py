@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+The reference ships no fixtures, golden vectors or recordings for its DSP path
+(SURVEY.md §4, §8c), so they are manufactured here: the reference's own
+src/filter.cpp, compiled unmodified from /root/reference by
+``make -C oracle ref`` (oracle/_ref/libref_filter.so, wrapped by
+oracle/ref_shim.cpp), is run on seeded synthetic inputs and its outputs are
+stored.  Every case is a multi-block run, so the inter-block state carry
+(src/filter.cpp:82,139,169; prev_I/prev_Q :100-101) is pinned too.
+
+Inputs are stored in the fixture (not re-generated), so the fixtures do not
+depend on numpy's RNG stream staying stable.  Each case is one
+``<name>.npz`` (plain arrays, loadable with allow_pickle=False);
+MANIFEST.json records the reference function, parameters, shapes, seed and
+sha256 of every file.
+
+Run in the build container (needs /root/reference):
+    make -C oracle ref && python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "3dy4-real-time-software-defined-radio-_amd"))
+
+from oracle import Reference  # noqa: E402
+from sdrhip.synth import fm_iq_u8, planar_from_u8  # noqa: E402
+
+SEED = 1234
+manifest: dict = {"generator": "tests/golden/make_golden.py",
+                  "reference": "src/filter.cpp compiled by oracle/Makefile (target ref)",
+                  "seed": SEED, "cases": {}}
+
+
+def save(name: str, func: str, params: dict, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    with open(path, "rb") as f:
+        digest = hashlib.sha256(f.read()).hexdigest()
+    manifest["cases"][name] = {"function": func, "params": params, "sha256": digest,
+                               "shapes": {k: list(np.shape(v)) for k, v in arrays.items()}}
+
+
+def main():
+    ref = Reference()
+    rng = np.random.default_rng(SEED)
+
+    # ---- taps (src/filter.cpp:14-49), the filters src/project.cpp:262-273 builds + the BASELINE configs
+    lpf_cases = {
+        "rf_mode0": (2.4e6, 100e3, 101, 1), "rf_mode1": (1.44e6, 100e3, 101, 1),
+        "rf_mode3": (1.92e6, 100e3, 101, 1), "audio_mode0": (240e3, 16e3, 101, 1),
+        "audio_mode1": (288e3, 16e3, 101, 1), "audio_mode2": (240e3 * 147, 16e3, 14847, 147),
+        "audio_mode3": (384e3 * 147, 16e3, 14847, 147), "cfg3_151pp": (240e3 * 147, 16e3, 22197, 147),
+        "cfg5_1024": (2.4e6, 100e3, 1024, 1),
+    }
+    bpf_cases = {"pilot_mode0": (240e3, 18.5e3, 19.5e3, 101, 1), "stereo_mode0": (240e3, 22e3, 54e3, 101, 1),
+                 "pilot_mode1": (288e3, 18.5e3, 19.5e3, 101, 1), "stereo_mode1": (288e3, 22e3, 54e3, 101, 1)}
+    taps = {}
+    arrays = {}
+    for k, a in lpf_cases.items():
+        taps[k] = ref.taps_lpf(*a)
+        arrays["lpf_" + k] = taps[k]
+    for k, a in bpf_cases.items():
+        taps[k] = ref.taps_bpf(*a)
+        arrays["bpf_" + k] = taps[k]
+    save("taps", "impulseResponseLPF/BPF",
+         {"lpf": {k: list(v) for k, v in lpf_cases.items()}, "bpf": {k: list(v) for k, v in bpf_cases.items()}},
+         **arrays)
+
+    # ---- front end: FIR+decimate I and Q, then demod, block after block (src/project.cpp:86-90)
+    def frontend_case(name, D, block, nblk, h, seed):
+        # never record a reference run that violates its own preconditions
+        # (n % D != 0 overflows y in downsampleBlockConvolveFIR: the output
+        # would be heap garbage, not a golden vector)
+        assert block % D == 0 and block >= 100
+        iq = fm_iq_u8(block * nblk, seed=seed)
+        I, Q = planar_from_u8(iq)
+        si, sq = np.zeros(100, np.float32), np.zeros(100, np.float32)
+        prev = np.zeros(2, np.float32)
+        yi_all, yq_all, dm_all, st = [], [], [], []
+        for b in range(nblk):
+            xi, xq = I[b * block:(b + 1) * block], Q[b * block:(b + 1) * block]
+            yi = ref.fir_decim(D, xi, h, si)
+            yq = ref.fir_decim(D, xq, h, sq)
+            dm = ref.fm_demod(yi, yq, prev)
+            yi_all.append(yi); yq_all.append(yq); dm_all.append(dm)
+            st.append(np.concatenate([si, sq, prev]))
+        save(name, "downsampleBlockConvolveFIR x2 + fmDemodArctan",
+             {"D": D, "block": block, "nblk": nblk, "ntaps": len(h), "state": 100, "seed": seed},
+             iq_u8=iq, h=h, yi=np.stack(yi_all), yq=np.stack(yq_all), demod=np.stack(dm_all), states=np.stack(st))
+
+    frontend_case("frontend_mode0", 10, 5120, 3, taps["rf_mode0"], SEED)
+    frontend_case("frontend_mode1", 5, 4100, 3, taps["rf_mode1"], SEED + 1)
+    # block == taps-1 == state size: the smallest block the reference handles
+    frontend_case("frontend_block100", 10, 100, 4, taps["rf_mode0"], SEED + 2)
+    # large block (beyond one GPU tile) at the BASELINE block size, 2 blocks
+    frontend_case("frontend_65540", 10, 65540, 2, taps["rf_mode0"], SEED + 3)
+
+    # ---- demod edge cases: zero envelope, single sample, prev carry (src/filter.cpp:85-102)
+    I = rng.standard_normal(257).astype(np.float32) * 0.5
+    Q = rng.standard_normal(257).astype(np.float32) * 0.5
+    I[[0, 5, 6, 100]] = 0.0
+    Q[[0, 5, 6, 100]] = 0.0
+    I[50], Q[50] = 1e-20, 0.0  # I^2+Q^2 underflows float -> 0 envelope branch
+    I[51], Q[51] = 3e-20, 1e-22  # tiny but nonzero in float after rounding? (pinned either way)
+    prev = np.array([0.25, -0.5], np.float32)
+    outs, prevs = [], []
+    segs = [(0, 1), (1, 200), (200, 257)]
+    for a, b in segs:
+        outs.append(ref.fm_demod(I[a:b], Q[a:b], prev))
+        prevs.append(prev.copy())
+    save("demod_edges", "fmDemodArctan", {"segments": segs, "prev0": [0.25, -0.5]},
+         I=I, Q=Q, prev0=np.array([0.25, -0.5], np.float32), out=np.concatenate(outs), prevs=np.stack(prevs))
+
+    # ---- stateful block FIR, D = 1 (src/filter.cpp:66-83): stereo BPFs, and the cfg5 1024-tap LPF
+    def block_case(name, h, ns, block, nblk, seed):
+        assert ns >= len(h) - 1 and block >= ns
+        x = np.random.default_rng(seed).standard_normal(block * nblk).astype(np.float32) * 0.3
+        st = np.zeros(ns, np.float32)
+        ys, sts = [], []
+        for b in range(nblk):
+            ys.append(ref.fir_block(x[b * block:(b + 1) * block], h, st))
+            sts.append(st.copy())
+        save(name, "blockConvolveFIR", {"ntaps": len(h), "state": ns, "block": block, "nblk": nblk, "seed": seed},
+             x=x, h=h, y=np.stack(ys), states=np.stack(sts))
+
+    block_case("fir_block_pilot", taps["pilot_mode0"], 100, 1000, 3, SEED + 10)
+    block_case("fir_block_stereo", taps["stereo_mode0"], 100, 5120, 2, SEED + 11)
+    block_case("fir_block_1024", taps["cfg5_1024"], 1023, 4096, 2, SEED + 12)
+
+    # ---- polyphase resampler (src/filter.cpp:142-173)
+    def resample_case(name, up, down, h, ns, block, nblk, seed):
+        assert (block * up) % down == 0 and (len(h) - 1) // up <= ns and block >= ns
+        x = np.random.default_rng(seed).standard_normal(block * nblk).astype(np.float32) * 0.3
+        st = np.zeros(ns, np.float32)
+        ys, sts = [], []
+        for b in range(nblk):
+            ys.append(ref.resample(up, down, x[b * block:(b + 1) * block], h, st))
+            sts.append(st.copy())
+        save(name, "resampleBlockConvolveFIR",
+             {"up": up, "down": down, "ntaps": len(h), "state": ns, "block": block, "nblk": nblk, "seed": seed},
+             x=x, h=h, y=np.stack(ys), states=np.stack(sts))
+
+    resample_case("resample_mode0", 1, 5, taps["audio_mode0"], 100, 5120, 3, SEED + 20)
+    resample_case("resample_mode2", 147, 800, taps["audio_mode2"], 100, 8000, 2, SEED + 21)
+    resample_case("resample_mode3", 147, 1280, taps["audio_mode3"], 100, 12800, 2, SEED + 22)
+    resample_case("resample_cfg3", 147, 800, taps["cfg3_151pp"], 150, 1600, 3, SEED + 23)
+    resample_case("resample_3_5", 3, 5, ref.taps_lpf(240e3 * 3, 16e3, 151, 3), 50, 500, 3, SEED + 24)
+
+    # ---- host-side rows: PLL, delay, mixer, add/sub, interleave, plain conv
+    x = np.random.default_rng(SEED + 30).standard_normal(2048).astype(np.float32) * 0.3
+    st = np.zeros(100, np.float32)
+    pf = ref.fir_block(x, taps["pilot_mode0"], st)
+    pll = np.array([1, 0, 0, 0, 0, 1], np.float32)
+    nco, plls = [], []
+    for a, b in ((0, 1024), (1024, 2048)):
+        nco.append(ref.fm_pll(pf[a:b], 19e3, 240e3, 2.0, 0.0, 0.01, pll))
+        plls.append(pll.copy())
+    dst = np.zeros(50, np.float32)
+    d1 = ref.delay_block(x[:1024], dst)
+    d2 = ref.delay_block(x[1024:], dst)
+    y = x[::-1].copy()
+    save("host_glue", "fmPLL/delayBlock/pointwise*/interleave/convolveFIR/downsample/upsample",
+         {"pll": [19e3, 240e3, 2.0, 0.0, 0.01], "delay_state": 50},
+         x=x, pilot=pf, nco=np.stack(nco), pll_states=np.stack(plls), delay=np.stack([d1, d2]), delay_state=dst,
+         mul=ref.pointwise_mul(x, y[:2000]), add=ref.pointwise_add(x, y), sub=ref.pointwise_sub(x, y),
+         inter=ref.interleave(x[:100], y[:100]), conv=ref.convolve_full(x[:300], taps["pilot_mode0"]),
+         down=ref.downsample(x[:303], 10), up=ref.upsample(x[:40], 3))
+
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    total = sum(os.path.getsize(os.path.join(HERE, n + ".npz")) for n in manifest["cases"])
+    print(f"wrote {len(manifest['cases'])} fixtures, {total / 1024:.0f} KiB")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""The C-ABI boundary, checked without a GPU: the library loads, exports
+exactly what include/sdr_hip.h declares, the drop-in library exports every
+filter.h symbol, and the host-side sizing/precondition logic matches the
+reference."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+FILTER_H_SYMBOLS = [  # include/filter.h:17-34 of the reference, as C++ signatures
+    "impulseResponseLPF(float, float, unsigned short, std::vector<float, std::allocator<float> >&, int)",
+    "convolveFIR(std::vector<float, std::allocator<float> >&, std::vector<float, std::allocator<float> > const&, "
+    "std::vector<float, std::allocator<float> > const&)",
+    "blockConvolveFIR(", "fmDemodArctan(", "downsample(", "upsample(", "downsampleBlockConvolveFIR(",
+    "resampleBlockConvolveFIR(", "impulseResponseBPF(", "fmPLL(", "delayBlock(", "pointwiseMultiply(",
+    "pointwiseAdd(", "pointwiseSubtract(", "interleave(",
+]
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-DC", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return [line.split(" ", 2)[2] for line in out.splitlines() if " T " in line]
+
+
+def test_header_matches_exports(built_lib):
+    sdrhip = built_lib
+    declared = sdrhip.header_symbols()
+    exported = {s for s in _exports(sdrhip.LIB_PATH) if s.startswith("sdr_")}
+    assert set(declared) == exported, (set(declared) ^ exported)
+    assert set(declared) == set(sdrhip.EXPORTED)  # the binding covers the whole ABI
+
+
+def test_dropin_exports_all_filter_h(built_lib):
+    ex = _exports(os.path.join(PKG, "libdy4filter_hip.so"))
+    for sym in FILTER_H_SYMBOLS:
+        assert any(e.startswith(sym) for e in ex), sym
+    # exactly the functions of filter.h, nothing else
+    assert len([e for e in ex if "(" in e]) == 15  # filter.h:17-34 declares 15 functions
+
+
+def test_dropin_links_the_hip_library(built_lib):
+    out = subprocess.run(["ldd", os.path.join(PKG, "libdy4filter_hip.so")], capture_output=True, text=True).stdout
+    assert "libsdrhip.so" in out
+
+
+def test_library_is_gfx950(built_lib):
+    """The embedded HIP fat binary carries a gfx950 code object."""
+    blob = open(built_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_resample_out_len_matches_reference_expression(built_lib, oracle):
+    for up, down, n in [(1, 5, 5120), (147, 800, 8000), (147, 1280, 12800), (147, 800, 65600), (3, 5, 500),
+                        (147, 800, 65536), (1, 8, 8192), (7, 3, 1001)]:
+        assert built_lib.resample_out_len(up, down, n) == oracle.resample_len(up, down, n)
+        assert built_lib.resample_out_len(up, down, n) == int(np.float32(np.float32(n) / np.float32(down))
+                                                               * np.float32(up))
+
+
+def test_context_without_gpu_fails_loudly(built_lib):
+    if built_lib.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(built_lib.SdrError):
+        built_lib.Context(0)
+
+
+def test_error_strings(built_lib):
+    L = built_lib.lib()
+    for code in (0, -1, -2, -3, -4):
+        assert L.sdr_strerror(code)
+    assert b"gfx950" in L.sdr_version()
+
+
+def test_dropin_builds_against_reference_project():
+    """oracle/_ref/project_hip is the reference's unmodified project.cpp
+    linked against the drop-in (built by `make -C oracle dropin` where the
+    reference is present)."""
+    path = os.path.join(REPO, "oracle", "_ref", "project_hip")
+    if not os.path.exists(path):
+        pytest.skip("drop-in project binary not built here")
+    out = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
+    assert "libsdrhip.so" in out
+    syms = subprocess.run(["nm", "-C", path], capture_output=True, text=True).stdout
+    assert "downsampleBlockConvolveFIR" in syms and "sdr_fir_decim_f32" in syms
+
+
+def test_taps_c_abi_bit_exact(built_lib, manifest):
+    """Coefficient design through the C ABI (host code, no GPU needed)."""
+    from conftest import assert_bits, load_golden
+
+    g = load_golden("taps")
+    params = manifest["cases"]["taps"]["params"]
+    for k, (Fs, Fc, T, U) in params["lpf"].items():
+        assert_bits(built_lib.taps_lpf(Fs, Fc, int(T), int(U)), g["lpf_" + k], f"lpf {k}")
+    for k, (Fs, Fb, Fe, T, U) in params["bpf"].items():
+        assert_bits(built_lib.taps_bpf(Fs, Fb, Fe, int(T), int(U)), g["bpf_" + k], f"bpf {k}")

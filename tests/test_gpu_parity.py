@@ -1,0 +1,285 @@
+"""GPU parity: the HIP kernels, called through the C ABI, against the golden
+fixtures of the compiled reference and against the oracle (the CPU
+restatement pinned by those fixtures).
+
+The bar is BIT-EXACT for every output and every carried state: the kernels
+reproduce the reference's fp32 operation order (products and sums rounded
+separately, taps in ascending order from 0.0f, double-precision envelope in
+the discriminator), so no tolerance is needed.  For sizes where the oracle
+would be too slow, size-independent properties are checked instead
+(stream/shard permutation invariance, block-size independence).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_bits, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _blocks(a, block, nblk):
+    return [a[b * block:(b + 1) * block] for b in range(nblk)]
+
+
+# ------------------------------------------------------------ golden, host API
+
+@pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
+def test_frontend_fused_golden(gpu_ctx, oracle, manifest, name):
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    I, Q = oracle.u8_to_planar(g["iq_u8"])
+    si, sq, prev = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
+    for b, (xi, xq) in enumerate(zip(_blocks(I, p["block"], p["nblk"]), _blocks(Q, p["block"], p["nblk"]))):
+        dm = gpu_ctx.frontend(p["D"], xi, xq, g["h"], si, sq, prev)
+        assert_bits(dm, g["demod"][b], f"{name} demod[{b}]")
+        assert_bits(np.concatenate([si, sq, prev]), g["states"][b], f"{name} states[{b}]")
+
+
+@pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
+def test_frontend_u8_golden(gpu_ctx, manifest, name):
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    si, sq, prev = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
+    for b, iq in enumerate(_blocks(g["iq_u8"], 2 * p["block"], p["nblk"])):
+        dm = gpu_ctx.frontend_u8(p["D"], iq, g["h"], si, sq, prev)
+        assert_bits(dm, g["demod"][b], f"{name} u8 demod[{b}]")
+        assert_bits(np.concatenate([si, sq, prev]), g["states"][b], f"{name} u8 states[{b}]")
+
+
+@pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_65540"])
+def test_fir_decim_and_demod_golden(gpu_ctx, oracle, manifest, name):
+    """The unfused calls, exactly as src/project.cpp:86-90 makes them."""
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    I, Q = oracle.u8_to_planar(g["iq_u8"])
+    si, sq, prev = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
+    for b in range(p["nblk"]):
+        sl = slice(b * p["block"], (b + 1) * p["block"])
+        yi = gpu_ctx.fir_decim(p["D"], I[sl], g["h"], si)
+        yq = gpu_ctx.fir_decim(p["D"], Q[sl], g["h"], sq)
+        assert_bits(yi, g["yi"][b], f"{name} yi[{b}]")
+        assert_bits(yq, g["yq"][b], f"{name} yq[{b}]")
+        dm = gpu_ctx.fm_demod(yi, yq, prev)
+        assert_bits(dm, g["demod"][b], f"{name} demod[{b}]")
+        assert_bits(np.concatenate([si, sq, prev]), g["states"][b], f"{name} states[{b}]")
+
+
+def test_demod_edges_golden(gpu_ctx, manifest):
+    g = load_golden("demod_edges")
+    prev = g["prev0"].copy()
+    outs = []
+    for i, (a, b) in enumerate(manifest["cases"]["demod_edges"]["params"]["segments"]):
+        outs.append(gpu_ctx.fm_demod(g["I"][a:b], g["Q"][a:b], prev))
+        assert_bits(prev, g["prevs"][i], f"prev[{i}]")
+    assert_bits(np.concatenate(outs), g["out"], "demod edges")
+
+
+@pytest.mark.parametrize("name", ["fir_block_pilot", "fir_block_stereo", "fir_block_1024"])
+def test_fir_block_golden(gpu_ctx, manifest, name):
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    st = np.zeros(p["state"], np.float32)
+    for b, x in enumerate(_blocks(g["x"], p["block"], p["nblk"])):
+        assert_bits(gpu_ctx.fir_block(x, g["h"], st), g["y"][b], f"{name} y[{b}]")
+        assert_bits(st, g["states"][b], f"{name} state[{b}]")
+
+
+@pytest.mark.parametrize("name", ["resample_mode0", "resample_mode2", "resample_mode3", "resample_cfg3",
+                                  "resample_3_5"])
+def test_resample_golden(gpu_ctx, manifest, name):
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    st = np.zeros(p["state"], np.float32)
+    for b, x in enumerate(_blocks(g["x"], p["block"], p["nblk"])):
+        assert_bits(gpu_ctx.resample(p["up"], p["down"], x, g["h"], st), g["y"][b], f"{name} y[{b}]")
+        assert_bits(st, g["states"][b], f"{name} state[{b}]")
+
+
+# ---------------------------------------------------- oracle, other shapes
+
+@pytest.mark.parametrize("D,ntaps,ns,n", [(10, 101, 100, 5120), (10, 101, 137, 5230), (5, 101, 100, 4100),
+                                           (1, 101, 100, 3000), (8, 101, 100, 8192), (3, 17, 40, 999),
+                                           (10, 64, 63, 640), (1, 1024, 1023, 4096), (4, 300, 320, 4000)])
+def test_fir_decim_vs_oracle(gpu_ctx, oracle, D, ntaps, ns, n):
+    """Tiled and generic kernels, odd state lengths, even/odd tap counts."""
+    rng = np.random.default_rng(D * 1000 + ntaps)
+    h = rng.standard_normal(ntaps).astype(np.float32) / ntaps
+    s_g = rng.standard_normal(ns).astype(np.float32)
+    s_o = s_g.copy()
+    for blk in range(3):
+        x = rng.standard_normal(n).astype(np.float32)
+        assert_bits(gpu_ctx.fir_decim(D, x, h, s_g), oracle.fir_decim(D, x, h, s_o), f"D={D} T={ntaps} blk {blk}")
+        assert_bits(s_g, s_o, "state")
+
+
+@pytest.mark.parametrize("up,down,ntaps,ns,n", [(147, 800, 22197, 150, 1600), (2, 3, 61, 30, 999),
+                                                 (3, 8, 301, 150, 1600), (5, 2, 100, 20, 400)])
+def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
+    rng = np.random.default_rng(up * 7 + down)
+    h = rng.standard_normal(ntaps).astype(np.float32) / 20
+    s_g = rng.standard_normal(ns).astype(np.float32)
+    s_o = s_g.copy()
+    for blk in range(2):
+        x = rng.standard_normal(n).astype(np.float32)
+        assert_bits(gpu_ctx.resample(up, down, x, h, s_g), oracle.resample(up, down, x, h, s_o), f"blk {blk}")
+        assert_bits(s_g, s_o, "state")
+
+
+# ------------------------------------------------------- batched device API
+
+def _fm_streams(nstreams, n, seed=5):
+    from sdrhip.synth import fm_iq_u8
+
+    return np.stack([fm_iq_u8(n, seed=seed + s) for s in range(nstreams)])
+
+
+@pytest.mark.parametrize("src", ["f32", "u8"])
+@pytest.mark.parametrize("D,n", [(10, 65540), (10, 5120), (5, 40960)])
+def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, src, D, n):
+    """nstreams independent streams x 3 consecutive blocks through the
+    device-resident batched call; every stream checked against the oracle."""
+    sdrhip = built_lib
+    nstreams, nblk = 6, 3
+    h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
+    iq = _fm_streams(nstreams, n * nblk)
+    nout = n // D
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_si = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros((nstreams, 100), np.float32))
+    d_sq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros((nstreams, 100), np.float32))
+    d_pi = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    d_pq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    out_stride = (nout + 3) // 4 * 4 + 4  # padded rows
+    d_out = sdrhip.DeviceArray(gpu_ctx, nstreams * out_stride * 4)
+    ors = [dict(si=np.zeros(100, np.float32), sq=np.zeros(100, np.float32), prev=np.zeros(2, np.float32))
+           for _ in range(nstreams)]
+    for b in range(nblk):
+        blk = iq[:, 2 * n * b:2 * n * (b + 1)]
+        if src == "u8":
+            d_iq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.ascontiguousarray(blk))
+            gpu_ctx.frontend_u8_dev(D, d_iq, n, nstreams, 2 * n, d_h, len(h), d_si, d_sq, 100, d_pi, d_pq, d_out,
+                                    out_stride)
+        else:
+            I = np.stack([oracle.u8_to_planar(blk[s])[0] for s in range(nstreams)])
+            Q = np.stack([oracle.u8_to_planar(blk[s])[1] for s in range(nstreams)])
+            d_I = sdrhip.DeviceArray.from_numpy(gpu_ctx, I)
+            d_Q = sdrhip.DeviceArray.from_numpy(gpu_ctx, Q)
+            gpu_ctx.frontend_dev(D, d_I, d_Q, n, nstreams, n, d_h, len(h), d_si, d_sq, 100, d_pi, d_pq, d_out,
+                                 out_stride)
+        gpu_ctx.synchronize()
+        got = d_out.download().reshape(nstreams, out_stride)[:, :nout]
+        for s in range(nstreams):
+            Is, Qs = oracle.u8_to_planar(blk[s])
+            want = oracle.frontend(D, Is, Qs, h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"])
+            assert_bits(got[s], want, f"stream {s} block {b}")
+        assert_bits(d_si.download().reshape(nstreams, 100), np.stack([o["si"] for o in ors]), "state_i")
+        assert_bits(d_sq.download().reshape(nstreams, 100), np.stack([o["sq"] for o in ors]), "state_q")
+        assert_bits(d_pi.download(), np.array([o["prev"][0] for o in ors], np.float32), "prev_i")
+        assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), "prev_q")
+
+
+def test_fir_decim_batched_misaligned_stride(gpu_ctx, oracle, built_lib):
+    """A stride that breaks 16-B row alignment takes the generic kernel: same bits."""
+    sdrhip = built_lib
+    rng = np.random.default_rng(3)
+    nstreams, n, stride = 3, 5120, 5123
+    h = load_golden("taps")["lpf_rf_mode0"]
+    x = rng.standard_normal((nstreams, stride)).astype(np.float32)
+    st = rng.standard_normal((nstreams, 100)).astype(np.float32)
+    d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_s = sdrhip.DeviceArray.from_numpy(gpu_ctx, st)
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * 513 * 4)
+    gpu_ctx.fir_decim_dev(10, d_x, n, nstreams, stride, d_h, 101, d_s, 100, d_y, 513)
+    gpu_ctx.synchronize()
+    y = d_y.download().reshape(nstreams, 513)[:, :512]
+    for s in range(nstreams):
+        so = st[s].copy()
+        assert_bits(y[s], oracle.fir_decim(10, x[s, :n], h, so), f"stream {s}")
+        assert_bits(d_s.download().reshape(nstreams, 100)[s], so, "state")
+
+
+def test_u8_to_planar_dev(gpu_ctx, oracle, built_lib):
+    sdrhip = built_lib
+    iq = _fm_streams(2, 10007 + 1, seed=9)[:, :2 * 10000]
+    d_iq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.ascontiguousarray(iq))
+    d_I = sdrhip.DeviceArray(gpu_ctx, 2 * 10000 * 4)
+    d_Q = sdrhip.DeviceArray(gpu_ctx, 2 * 10000 * 4)
+    gpu_ctx.u8_to_planar_dev(d_iq, 10000, 2, 20000, d_I, d_Q, 10000)
+    gpu_ctx.synchronize()
+    for s in range(2):
+        I, Q = oracle.u8_to_planar(iq[s])
+        assert_bits(d_I.download().reshape(2, 10000)[s], I)
+        assert_bits(d_Q.download().reshape(2, 10000)[s], Q)
+
+
+# ------------------------------------------- full BASELINE sizes: properties
+
+def test_full_size_stream_permutation_and_spotcheck(gpu_ctx, oracle, built_lib):
+    """BASELINE config 2 at full size (1024 x 65,540-pair blocks, device
+    synthetic input): (a) running the streams in a different order/grouping
+    gives identical bits per stream (no cross-stream leakage, the property
+    multi-GPU sharding relies on); (b) a sample of streams equals the oracle."""
+    sdrhip = built_lib
+    nstreams, n, D = 1024, 65540, 10
+    nout = n // D
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_iq = sdrhip.DeviceArray(gpu_ctx, nstreams * 2 * n)
+    gpu_ctx.synth_fm_u8_dev(d_iq, n, nstreams, 2 * n, seed=77)
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+
+    def run(streams):
+        k = len(streams)
+        d_si = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros((k, 100), np.float32))
+        d_sq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros((k, 100), np.float32))
+        d_pi = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(k, np.float32))
+        d_pq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(k, np.float32))
+        d_out = sdrhip.DeviceArray(gpu_ctx, k * nout * 4 + 16)
+        # contiguous runs of streams are one batched launch each
+        s0 = streams[0]
+        assert list(streams) == list(range(s0, s0 + k))
+        gpu_ctx.frontend_u8_dev(D, d_iq.ptr + s0 * 2 * n, n, k, 2 * n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq,
+                                d_out, nout)
+        gpu_ctx.synchronize()
+        return d_out.download(count=k * nout).reshape(k, nout)
+
+    full = run(list(range(nstreams)))
+    half = np.concatenate([run(list(range(512, 1024))), run(list(range(0, 512)))])
+    assert_bits(np.concatenate([half[512:], half[:512]]), full, "regrouped streams")
+    iq_host = d_iq.download(np.uint8).reshape(nstreams, 2 * n)
+    for s in (0, 1, 511, 777, 1023):
+        I, Q = oracle.u8_to_planar(iq_host[s])
+        want = oracle.frontend(D, I, Q, h, np.zeros(100, np.float32), np.zeros(100, np.float32),
+                               np.zeros(2, np.float32))
+        assert_bits(full[s], want, f"stream {s}")
+
+
+def test_block_size_independence_gpu(gpu_ctx, oracle):
+    """One stream as one 655,400-pair block == the same samples as 10 blocks."""
+    from sdrhip.synth import fm_planar
+
+    I, Q = fm_planar(655400, seed=11)
+    h = load_golden("taps")["lpf_rf_mode0"]
+    z = lambda k: np.zeros(k, np.float32)  # noqa: E731
+    whole = gpu_ctx.frontend(10, I, Q, h, z(100), z(100), z(2))
+    si, sq, pv = z(100), z(100), z(2)
+    parts = [gpu_ctx.frontend(10, I[a:a + 65540], Q[a:a + 65540], h, si, sq, pv) for a in range(0, 655400, 65540)]
+    assert_bits(np.concatenate(parts), whole, "blocked vs whole")
+
+
+# ----------------------------------------------------------- preconditions
+
+def test_preconditions_are_errors(gpu_ctx, built_lib):
+    sdrhip = built_lib
+    h = np.ones(101, np.float32)
+    with pytest.raises(sdrhip.SdrError) as e:  # reference: heap overflow at filter.cpp:132
+        gpu_ctx.fir_decim(10, np.zeros(65536, np.float32), h, np.zeros(100, np.float32))
+    assert e.value.code == sdrhip.SDR_EINVAL and "multiple" in str(e.value)
+    with pytest.raises(sdrhip.SdrError):  # state shorter than taps-1: reads before state
+        gpu_ctx.fir_block(np.zeros(1000, np.float32), h, np.zeros(50, np.float32))
+    with pytest.raises(sdrhip.SdrError):  # block shorter than the state: state.assign UB
+        gpu_ctx.fir_decim(10, np.zeros(50, np.float32), h, np.zeros(100, np.float32))
+    with pytest.raises(sdrhip.SdrError):  # resampler y overflow (n*L % M != 0)
+        gpu_ctx.resample(147, 800, np.zeros(65536, np.float32), np.ones(22197, np.float32),
+                         np.zeros(150, np.float32))
+    with pytest.raises(sdrhip.SdrError):  # empty demod block: reference reads I[-1]
+        gpu_ctx.fm_demod(np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(2, np.float32))
