@@ -408,8 +408,8 @@ int sdr_u8_to_planar_dev(sdr_ctx* c, const uint8_t* iq, long long npairs, int ns
   int rc = enter(c);
   if (rc) return rc;
   if (!iq || !I || !Q || npairs <= 0 || nstreams < 1) return fail(c, SDR_EINVAL, "bad u8_to_planar arguments");
-  if (!vec_ok(iq, iq_stride, 1, nstreams) || !vec_ok(I, x_stride, 4, nstreams) || !vec_ok(Q, x_stride, 4, nstreams))
-    return fail(c, SDR_EINVAL, "u8_to_planar needs 16-B aligned rows");
+  if (!vec_ok(iq, iq_stride, 1, nstreams, 8) || !vec_ok(I, x_stride, 4, nstreams) || !vec_ok(Q, x_stride, 4, nstreams))
+    return fail(c, SDR_EINVAL, "u8_to_planar needs 8-B aligned u8 rows and 16-B aligned float rows");
   hipError_t e = sdr::launch_u8_to_planar(iq, npairs, nstreams, iq_stride, I, Q, x_stride, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "u8_to_planar launch");
   return SDR_OK;

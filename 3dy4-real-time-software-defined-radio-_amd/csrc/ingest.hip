@@ -8,31 +8,22 @@
 namespace sdr {
 namespace {
 
-// 8 pairs (16 bytes) per thread: one 16-B load, two 32-B stores.
+// 4 pairs (8 bytes) per thread: one 8-B load, two 16-B stores.
 __global__ __launch_bounds__(kWG) void u8_to_planar(const uint8_t* __restrict__ iq, long long npairs,
                                                     long long iq_stride, float* __restrict__ I,
                                                     float* __restrict__ Q, long long x_stride) {
   const int s = blockIdx.y;
-  const long long g = ((long long)blockIdx.x * kWG + threadIdx.x) * 8;
+  const long long g = ((long long)blockIdx.x * kWG + threadIdx.x) * 4;
   if (g >= npairs) return;
   const uint8_t* src = iq + (long long)s * iq_stride + 2 * g;
   float* di = I + (long long)s * x_stride + g;
   float* dq = Q + (long long)s * x_stride + g;
-  if (g + 8 <= npairs) {
-    const uint4 b = *reinterpret_cast<const uint4*>(src);
-    const uint32_t w[4] = {b.x, b.y, b.z, b.w};
-    float vi[8], vq[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      vi[2 * k] = u8_to_f32(w[k] & 0xffu);
-      vq[2 * k] = u8_to_f32((w[k] >> 8) & 0xffu);
-      vi[2 * k + 1] = u8_to_f32((w[k] >> 16) & 0xffu);
-      vq[2 * k + 1] = u8_to_f32(w[k] >> 24);
-    }
-    reinterpret_cast<float4*>(di)[0] = make_float4(vi[0], vi[1], vi[2], vi[3]);
-    reinterpret_cast<float4*>(di)[1] = make_float4(vi[4], vi[5], vi[6], vi[7]);
-    reinterpret_cast<float4*>(dq)[0] = make_float4(vq[0], vq[1], vq[2], vq[3]);
-    reinterpret_cast<float4*>(dq)[1] = make_float4(vq[4], vq[5], vq[6], vq[7]);
+  if (g + 4 <= npairs) {
+    const uint2 b = *reinterpret_cast<const uint2*>(src);
+    *reinterpret_cast<float4*>(di) = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu),
+                                                 u8_to_f32(b.y & 0xffu), u8_to_f32((b.y >> 16) & 0xffu));
+    *reinterpret_cast<float4*>(dq) = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24),
+                                                 u8_to_f32((b.y >> 8) & 0xffu), u8_to_f32(b.y >> 24));
   } else {
     for (long long k = 0; g + k < npairs; ++k) {
       di[k] = u8_to_f32(src[2 * k]);
@@ -78,7 +69,7 @@ __global__ __launch_bounds__(kWG) void synth_fm_u8(uint8_t* __restrict__ iq, lon
 
 hipError_t launch_u8_to_planar(const uint8_t* iq, long long npairs, int nstreams, long long iq_stride, float* I,
                                float* Q, long long x_stride, hipStream_t st) {
-  const long long threads = (npairs + 7) / 8;
+  const long long threads = (npairs + 3) / 4;
   hipLaunchKernelGGL(u8_to_planar, dim3((unsigned)((threads + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0,
                      st, iq, npairs, iq_stride, I, Q, x_stride);
   return hipGetLastError();

@@ -114,8 +114,9 @@ int sdr_frontend_u8(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs, co
                     float *state_i, float *state_q, int ns, float *prev_i, float *prev_q, float *demod);
 
 /* -------------------------------- device-resident, batched, stream-ordered -- */
-/* Pointers 16-byte aligned and strides multiples of 4 elements (the kernels
- * stream 16-B vectors); otherwise SDR_EINVAL. */
+/* The tiled kernels stream 16-B vectors (8-B for u8 input): inputs whose
+ * stream rows are not so aligned run on the generic kernel instead -- same
+ * bits, lower throughput.  Output rows of any alignment are accepted. */
 int sdr_fir_decim_f32_dev(sdr_ctx *ctx, int D, const float *x, long long n, int nstreams, long long x_stride,
                           const float *h, int ntaps, float *state, int ns, float *y, long long y_stride);
 int sdr_fir_block_f32_dev(sdr_ctx *ctx, const float *x, long long n, int nstreams, long long x_stride,

@@ -9,9 +9,6 @@ import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 from conftest import ORACLE_DIR, PKG, assert_bits
 
@@ -26,6 +23,8 @@ def _free_port():
 
 def _worker(rank, world, port, q):
     import sys
+
+    import torch.distributed as dist
 
     sys.path[:0] = [PKG, ORACLE_DIR]
     from oracle import Oracle
@@ -75,6 +74,8 @@ def _worker(rank, world, port, q):
 
 
 def test_sharded_equals_single_process(oracle):
+    import torch.multiprocessing as mp
+
     from sdrhip.shard import stream_ranks
     from sdrhip.synth import fm_planar
 
