@@ -75,11 +75,20 @@ __device__ __forceinline__ float in_at(const float* x, const uint8_t* iq, int c,
 }
 
 // Element of the tile span at position p: x~[p], zero outside [-ns, n).
+// A guarded load (exec-masked), no branches around it.
 template <Src SRC>
 __device__ __forceinline__ float edge_at(const float* x, const uint8_t* iq, int c, const float* st, int ns,
                                          long long n, long long p) {
-  if (p < 0) return p >= -ns ? st[ns + p] : 0.0f;
-  return p < n ? in_at<SRC>(x, iq, c, p) : 0.0f;
+  const bool in_state = p < 0;
+  const bool valid = p >= -ns && p < n;
+  float v = 0.0f;
+  if constexpr (SRC == Src::F32) {
+    const float* src = in_state ? st + (ns + p) : x + p;
+    if (valid) v = *src;
+  } else {
+    if (valid) v = in_state ? st[ns + p] : u8_to_f32(iq[2 * p + c]);
+  }
+  return v;
 }
 
 template <int D, int T, int R, int NCH, bool DEMOD, Src SRC>
@@ -145,28 +154,38 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
       }
     }
   }
-  if (pb >= 0 && pb + G::LDS_LEN <= n) {
-    // interior tile: 16-B (f32) / 8-B (u8) coalesced vector loads, all
-    // issued before the first LDS store
+  {
+    // 16-B (f32) / 8-B (u8) coalesced vector loads for every chunk inside
+    // the block; the few chunks that straddle its start (old state) or end
+    // (zeros, never reaching a stored output) take four guarded scalar
+    // loads instead.  Every load is issued before the first LDS store.
     constexpr int FULL = G::LDS4 / kWG, REM = G::LDS4 % kWG;
     float4 v0[FULL + 1], v1[FULL + 1];
     auto load4 = [&](int i, float4& a0, float4& a1) {
       const long long p = pb + 4LL * i;
-      if constexpr (SRC == Src::F32) {
-        a0 = *reinterpret_cast<const float4*>(x0 + p);
-        if (NCH == 2) a1 = *reinterpret_cast<const float4*>(x1 + p);
+      if (p >= 0 && p + 4 <= n) {
+        if constexpr (SRC == Src::F32) {
+          a0 = *reinterpret_cast<const float4*>(x0 + p);
+          if (NCH == 2) a1 = *reinterpret_cast<const float4*>(x1 + p);
+        } else {
+          const uint2 b = *reinterpret_cast<const uint2*>(iq + 2 * p);
+          a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
+                           u8_to_f32((b.y >> 16) & 0xffu));
+          a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
+                           u8_to_f32(b.y >> 24));
+        }
       } else {
-        const uint2 b = *reinterpret_cast<const uint2*>(iq + 2 * p);
-        a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
-                         u8_to_f32((b.y >> 16) & 0xffu));
-        a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
-                         u8_to_f32(b.y >> 24));
+        a0 = make_float4(edge_at<SRC>(x0, iq, 0, st0, ns, n, p), edge_at<SRC>(x0, iq, 0, st0, ns, n, p + 1),
+                         edge_at<SRC>(x0, iq, 0, st0, ns, n, p + 2), edge_at<SRC>(x0, iq, 0, st0, ns, n, p + 3));
+        if (NCH == 2)
+          a1 = make_float4(edge_at<SRC>(x1, iq, 1, st1, ns, n, p), edge_at<SRC>(x1, iq, 1, st1, ns, n, p + 1),
+                           edge_at<SRC>(x1, iq, 1, st1, ns, n, p + 2), edge_at<SRC>(x1, iq, 1, st1, ns, n, p + 3));
       }
     };
 #pragma unroll
     for (int it = 0; it < FULL; ++it) load4(tid + it * kWG, v0[it], v1[it]);
-    // the ragged last row: clamp the index (a redundant in-bounds load) so
-    // every register is defined and the arrays stay in VGPRs
+    // the ragged last row: clamp the index (a redundant load) so every
+    // register is defined and the arrays stay in VGPRs
     const int il = tid < REM ? tid + FULL * kWG : FULL * kWG - 1;
     if (REM) load4(il, v0[FULL], v1[FULL]);
 #pragma unroll
@@ -178,15 +197,6 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
     if (REM && tid < REM) {
       *reinterpret_cast<float4*>(lds0 + 4 * il) = v0[FULL];
       if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * il) = v1[FULL];
-    }
-  } else {
-    // first / last tile of a stream: element-wise, with the state before
-    // the block and zeros past its end (zeros never reach a stored output)
-#pragma unroll 1
-    for (int i = tid; i < G::LDS_LEN; i += kWG) {
-      const long long p = pb + i;
-      lds0[i] = edge_at<SRC>(x0, iq, 0, st0, ns, n, p);
-      if (NCH == 2) lds1[i] = edge_at<SRC>(x1, iq, 1, st1, ns, n, p);
     }
   }
   __syncthreads();

@@ -156,8 +156,11 @@ def main():
 
     cfg = CONFIGS[args.config]
     ctx = sdrhip.Context(local)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)  # kernels and torch events on one stream
+    # one dedicated (non-null) HIP stream shared by torch and the library, so
+    # torch.cuda.Event timestamps bracket exactly the kernels we launch
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
 
     S, n, T = cfg["streams"], cfg["n"], cfg["ntaps"]
     seed = 1234 + 7919 * rank

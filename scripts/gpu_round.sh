@@ -27,4 +27,16 @@ export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o bench \
   -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof rc=$rc"; find "$OUT/prof" -name '*stats*' | head
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+
+# HBM traffic: one counter per pass (FETCH_SIZE, then WRITE_SIZE)
+if [ -n "${PMC:-}" ]; then
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_$ctr" -o pmc \
+      -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2>> "$OUT/prof.err"
+    rc=$?; echo "pmc $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  python scripts/pmc_traffic.py "$(find $OUT/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1)" \
+    "$(find $OUT/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)" fir_tile "$OUT/traffic_cfg2.json"
+fi
+exit 0
