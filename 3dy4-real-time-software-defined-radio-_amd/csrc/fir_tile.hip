@@ -27,6 +27,9 @@
 //     the demodulated stream: decimated I/Q never touch HBM.
 //   * state carry: only the first tile of a stream reads `state`/`prev`, so
 //     that workgroup alone rewrites them after its reads -- no second kernel.
+#include <cstdio>
+#include <cstdlib>
+
 #include "sdr_common.hpp"
 
 #pragma clang fp contract(off)
@@ -38,17 +41,18 @@ namespace {
 // the discriminator, lane 0 of every wave re-derives the R outputs just
 // before its wave's span (E = R), so each wave is self-contained (no
 // cross-wave hand-over, no barrier after the fill) at a 1/64 compute cost.
-template <int D, int T, int R, bool DEMOD>
+template <int D, int T, int R, bool DEMOD, int NW = 4>
 struct Geom {
+  static constexpr int NTH = 64 * NW;                               // threads per workgroup
   static_assert((D * R) % 4 == 0, "lane windows must start on 16-B boundaries");
   static constexpr int E = DEMOD ? R : 0;                          // overlap outputs per wave
   static constexpr int WADV = 64 * R - E;                          // new outputs per wave
-  static constexpr int ADV = 4 * WADV;                             // new outputs per tile
+  static constexpr int ADV = NW * WADV;                            // new outputs per tile
   static constexpr int HALO = (T - 1 + 3) / 4 * 4;                 // (T-1) rounded up to a float4
   static constexpr int SPAN = HALO + D * (R - 1) + 1;              // positions one lane reads
   static constexpr int NCHUNK = (SPAN + 3) / 4;                    // float4 chunks per lane window
   static constexpr int SPAN4 = 4 * NCHUNK;                         // tap row length
-  static constexpr int LDS_LEN = D * (3 * WADV + 63 * R) + SPAN4;  // floats per channel
+  static constexpr int LDS_LEN = D * ((NW - 1) * WADV + 63 * R) + SPAN4;  // floats per channel
   static constexpr int LDS4 = LDS_LEN / 4;
   static constexpr int TAIL = (T + 3) / 4 * 4;                     // prev_* recompute strip
   // LDS floats: channels, tap rows, two tail strips
@@ -91,9 +95,10 @@ __device__ __forceinline__ float edge_at(const float* x, const uint8_t* iq, int 
   return v;
 }
 
-template <int D, int T, int R, int NCH, bool DEMOD, Src SRC>
-__global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __restrict__ h) {
-  using G = Geom<D, T, R, DEMOD>;
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC>
+__global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  constexpr int NTH = G::NTH;
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
   static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
 
@@ -106,8 +111,13 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int s = blockIdx.x / a.tiles_per_stream;
-  const int t = blockIdx.x - s * a.tiles_per_stream;
+  // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch),
+  // so give each XCD a contiguous run of tiles -- neighbouring tiles of a
+  // stream then re-read each other's halo from the same L2.  Speed only.
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  const unsigned lin = (nb % 8u == 0u) ? (b % 8u) * (nb / 8u) + b / 8u : b;
+  const int s = (int)(lin / (unsigned)a.tiles_per_stream);
+  const int t = (int)(lin - (unsigned)s * (unsigned)a.tiles_per_stream);
   const long long n = a.n;
   const long long nout = n / D;
   const long long m_start = (long long)t * G::ADV - G::E;     // first output computed by the tile
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
     }
   }
   // tap rows: htab[r][w] = h[HALO + D*r - w] (0 where that k is not a tap)
-  for (int i = tid; i < R * G::SPAN4; i += kWG) {
+  for (int i = tid; i < R * G::SPAN4; i += NTH) {
     const int r = i / G::SPAN4, w = i - r * G::SPAN4;
     const int k = G::HALO + D * r - w;
     htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
@@ -147,7 +157,7 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
       // the T inputs of the block's last decimated sample (prev_* source);
       // D*(nout-1) - k >= -(T-1) >= -ns, so the old state covers p < 0
       const long long P = (long long)D * (nout - 1);
-      for (int k = tid; k < T; k += kWG) {
+      for (int k = tid; k < T; k += NTH) {
         const long long p = P - k;
         tail0[k] = p < 0 ? st0[ns + p] : in_at<SRC>(x0, iq, 0, p);
         tail1[k] = p < 0 ? st1[ns + p] : in_at<SRC>(x1, iq, 1, p);
@@ -159,7 +169,7 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
     // the block; the few chunks that straddle its start (old state) or end
     // (zeros, never reaching a stored output) take four guarded scalar
     // loads instead.  Every load is issued before the first LDS store.
-    constexpr int FULL = G::LDS4 / kWG, REM = G::LDS4 % kWG;
+    constexpr int FULL = G::LDS4 / NTH, REM = G::LDS4 % NTH;
     float4 v0[FULL + 1], v1[FULL + 1];
     auto load4 = [&](int i, float4& a0, float4& a1) {
       const long long p = pb + 4LL * i;
@@ -183,14 +193,14 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
       }
     };
 #pragma unroll
-    for (int it = 0; it < FULL; ++it) load4(tid + it * kWG, v0[it], v1[it]);
+    for (int it = 0; it < FULL; ++it) load4(tid + it * NTH, v0[it], v1[it]);
     // the ragged last row: clamp the index (a redundant load) so every
     // register is defined and the arrays stay in VGPRs
-    const int il = tid < REM ? tid + FULL * kWG : FULL * kWG - 1;
+    const int il = tid < REM ? tid + FULL * NTH : FULL * NTH - 1;
     if (REM) load4(il, v0[FULL], v1[FULL]);
 #pragma unroll
     for (int it = 0; it < FULL; ++it) {
-      const int i = tid + it * kWG;
+      const int i = tid + it * NTH;
       *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[it];
       if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[it];
     }
@@ -342,7 +352,7 @@ __global__ __launch_bounds__(kWG) void fir_tile(FirLaunch a, const float* __rest
       }
     }
     // state <- last ns input samples (src/filter.cpp:139)
-    for (int j = tid; j < ns; j += kWG) {
+    for (int j = tid; j < ns; j += NTH) {
       const long long p = n - ns + j;
       st0[j] = in_at<SRC>(x0, iq, 0, p);
       if (NCH == 2) st1[j] = in_at<SRC>(x1, iq, 1, p);
@@ -421,57 +431,94 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 }
 
 // ------------------------------------------------------------ dispatch ----
-template <int D, int T, int R, int NCH, bool DEMOD, Src SRC>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
-  using G = Geom<D, T, R, DEMOD>;
+  using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
   const long long nout = a.n / D;
   a.tiles_per_stream = (int)((nout + G::ADV - 1) / G::ADV);
   const size_t lds = (size_t)G::SMEM * sizeof(float);
   const long long blocks = (long long)a.tiles_per_stream * a.nstreams;
   if (blocks <= 0 || blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((fir_tile<D, T, R, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(kWG), lds, st, a, h);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a,
+                     h);
   return hipGetLastError();
 }
 
-// Fast-path table.  R is chosen so that D*R is a multiple of 4 (aligned lane
-// windows) and the LDS footprint allows >= 2 workgroups per CU.
+// Fast-path table: (R outputs per lane, NW waves per workgroup) per decimation
+// factor.  D*R must be a multiple of 4 (aligned lane windows).  The default
+// per D is the measured best on MI355X; SDR_FIR_VARIANT=<R>x<NW>
+// (e.g. "2x1") overrides it for experiments.
+struct Variant {
+  int R, NW;
+};
+
+Variant variant_for(int D, bool demod) {
+  static const char* env = std::getenv("SDR_FIR_VARIANT");
+  if (env) {
+    int r = 0, w = 0;
+    if (std::sscanf(env, "%dx%d", &r, &w) == 2) {
+      const Variant v{r, w};
+      const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
+                         (D == 5 && r == 4 && (w == 1 || w == 4)) ||
+                         (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
+      if (known) return v;
+    }
+  }
+  switch (D) {
+    case 10: return {2, 1};
+    case 5: return {4, 1};
+    case 1: return {4, 1};
+    default: return {0, 0};
+  }
+}
+
+// Runtime twin of Geom: only tile 0 may read the carried state, i.e. tile
+// 1's span must start at p >= 0.
+bool geometry_ok(int D, int T, int ns, bool demod, Variant v) {
+  if (v.R == 0 || ns < T - 1) return false;
+  const int halo = (T - 1 + 3) / 4 * 4;
+  const int E = demod ? v.R : 0;
+  const long long adv = (long long)v.NW * (64 * v.R - E);
+  return (long long)D * (adv - E) - halo >= 0;
+}
+
 template <int NCH, bool DEMOD, Src SRC>
 hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, bool* handled) {
   *handled = true;
+  const Variant v = variant_for(a.D, DEMOD);
+  const int key = a.D * 10000 + v.R * 100 + v.NW;
   if (a.ntaps == 101) {
-    switch (a.D) {
-      case 10: return run_tile<10, 101, 2, NCH, DEMOD, SRC>(a, h, st);
-      case 5: return run_tile<5, 101, 4, NCH, DEMOD, SRC>(a, h, st);
-      case 1:
-        if constexpr (!DEMOD) return run_tile<1, 101, 4, NCH, DEMOD, SRC>(a, h, st);
-        break;
+    switch (key) {
+      case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC>(a, h, st);
+      case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC>(a, h, st);
+      case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st);
+      case 100402: return run_tile<10, 101, 4, 2, NCH, DEMOD, SRC>(a, h, st);
+      case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st);
+      case 50404: return run_tile<5, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st);
       default: break;
+    }
+    if constexpr (!DEMOD && NCH == 1) {
+      switch (key) {
+        case 10401: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st);
+        case 10404: return run_tile<1, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st);
+        case 10801: return run_tile<1, 101, 8, 1, NCH, DEMOD, SRC>(a, h, st);
+        default: break;
+      }
     }
   }
   *handled = false;
   return hipSuccess;
 }
 
-// Only tile 0 may touch the carried state: tile 1's span must start at p >= 0.
-template <int D, int T, int R, bool DEMOD>
-constexpr bool tile_ok(int ns) {
-  using G = Geom<D, T, R, DEMOD>;
-  return ns >= T - 1 && (long long)D * (G::ADV - G::E) - G::HALO >= 0;
-}
-
 }  // namespace
 
 bool fir_has_fast_path(int D, int ntaps, int ns, int nch, bool demod, Src src) {
-  if (ntaps != 101 || ns < ntaps - 1) return false;
-  if (src == Src::U8 && nch != 2) return false;
-  if (demod && nch != 2) return false;
-  switch (D) {
-    case 10: return demod ? tile_ok<10, 101, 2, true>(ns) : tile_ok<10, 101, 2, false>(ns);
-    case 5: return demod ? tile_ok<5, 101, 4, true>(ns) : tile_ok<5, 101, 4, false>(ns);
-    case 1: return !demod && tile_ok<1, 101, 4, false>(ns);
-    default: return false;
-  }
+  if (ntaps != 101) return false;
+  if (src == Src::U8 && (nch != 2 || !demod)) return false;
+  if (demod != (nch == 2)) return false;  // instantiated: fused 2-channel, or 1-channel FIR
+  if (D != 10 && D != 5 && !(D == 1 && !demod)) return false;
+  return geometry_ok(D, ntaps, ns, demod, variant_for(D, demod));
 }
 
 hipError_t launch_demod(const float* I, const float* Q, long long n, int nstreams, long long stride, float* prev_i,
@@ -493,10 +540,8 @@ hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, S
       e = dispatch_tile<2, true, Src::U8>(a, h, st, &handled);
     } else if (demod) {
       e = dispatch_tile<2, true, Src::F32>(a, h, st, &handled);
-    } else if (nch == 1) {
-      e = dispatch_tile<1, false, Src::F32>(a, h, st, &handled);
     } else {
-      e = dispatch_tile<2, false, Src::F32>(a, h, st, &handled);
+      e = dispatch_tile<1, false, Src::F32>(a, h, st, &handled);
     }
     if (handled) return e;
   }
