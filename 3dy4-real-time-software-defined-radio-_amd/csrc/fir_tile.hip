@@ -11,22 +11,23 @@
 // rounded fp32 divide.
 //
 // Tile kernel structure (fir_tile):
-//   * one 256-thread workgroup = one tile of 256*R consecutive output samples
-//     of one stream; lane l owns outputs R*l .. R*l+R-1 of the tile;
-//   * the tile's input span (D*256*R samples plus a (T-1)-sample halo, i.e.
-//     overlap-save) is staged once into LDS with 16-B coalesced loads; the
-//     halo is re-read from the neighbouring tile's span (L2/MALL), or, for
-//     the first tile of a stream, from the carried `state`;
-//   * every lane then slides down its own D*R-aligned window of the tile in
-//     16-B ds_read_b128 chunks (stride D*R dwords across lanes -- 20 dwords
-//     for D=10, R=2 -- conflict-free) and accumulates all R outputs of both
-//     I and Q channels in registers; tap k is a compile-time index, so the
-//     taps are scalar (SGPR) operands loaded once per wave;
-//   * fused launches apply the discriminator in registers (prev sample via a
-//     wave shuffle / an LDS hand-over between the four waves) and write only
-//     the demodulated stream: decimated I/Q never touch HBM.
-//   * state carry: only the first tile of a stream reads `state`/`prev`, so
-//     that workgroup alone rewrites them after its reads -- no second kernel.
+//   * a tile = NW waves x 64 lanes x R consecutive output samples of one
+//     stream; its input span (D*64*NW*R samples plus a (T-1)-sample halo --
+//     overlap-save) is staged in LDS with 16-B coalesced loads.  The halo of
+//     a stream's first tile is the carried `state`;
+//   * every lane slides down its own D*R-aligned window of the tile in 16-B
+//     ds_read_b128 chunks (lane stride D*R dwords, 20 for D=10 R=2:
+//     conflict-free) and keeps all R outputs of I and Q in registers; the
+//     taps come from per-output LDS rows read as wave-wide broadcasts;
+//   * fused launches apply the discriminator in registers and write only the
+//     demodulated stream: decimated I/Q never touch HBM.  Lane 0 of each wave
+//     re-derives the R outputs before its span (E = R) so waves never wait on
+//     each other;
+//   * persistent workgroups walk a contiguous run of tiles; the loads of
+//     tile i+1 are issued into registers before tile i is computed, so each
+//     wave always has HBM reads in flight (software pipelining);
+//   * state carry: only the first tile of a stream reads `state`/`prev`;
+//     the workgroup that owns it rewrites them after its reads -- one kernel.
 #include <cstdio>
 #include <cstdlib>
 
@@ -37,11 +38,7 @@
 namespace sdr {
 namespace {
 
-// Tile geometry.  A workgroup computes 4 waves x 64 lanes x R outputs; with
-// the discriminator, lane 0 of every wave re-derives the R outputs just
-// before its wave's span (E = R), so each wave is self-contained (no
-// cross-wave hand-over, no barrier after the fill) at a 1/64 compute cost.
-template <int D, int T, int R, bool DEMOD, int NW = 4>
+template <int D, int T, int R, bool DEMOD, int NW>
 struct Geom {
   static constexpr int NTH = 64 * NW;                               // threads per workgroup
   static_assert((D * R) % 4 == 0, "lane windows must start on 16-B boundaries");
@@ -54,6 +51,7 @@ struct Geom {
   static constexpr int SPAN4 = 4 * NCHUNK;                         // tap row length
   static constexpr int LDS_LEN = D * ((NW - 1) * WADV + 63 * R) + SPAN4;  // floats per channel
   static constexpr int LDS4 = LDS_LEN / 4;
+  static constexpr int FULL = LDS4 / NTH, REM = LDS4 % NTH;        // staging rows per thread
   static constexpr int TAIL = (T + 3) / 4 * 4;                     // prev_* recompute strip
   // LDS floats: channels, tap rows, two tail strips
   static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4 + 2 * TAIL;
@@ -95,6 +93,101 @@ __device__ __forceinline__ float edge_at(const float* x, const uint8_t* iq, int 
   return v;
 }
 
+// Where one tile lives.
+struct TileRef {
+  int s;              // stream
+  int t;              // tile within the stream
+  long long m_start;  // first output the tile computes (includes the wave overlap)
+  long long pb;       // stream position of LDS index 0
+  const float* x0;
+  const float* x1;
+  const uint8_t* iq;
+  float* st0;
+  float* st1;
+};
+
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ __forceinline__ TileRef tile_ref(const FirLaunch& a, int lin) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  TileRef r;
+  r.s = lin / a.tiles_per_stream;
+  r.t = lin - r.s * a.tiles_per_stream;
+  r.m_start = (long long)r.t * G::ADV - G::E;
+  r.pb = (long long)D * r.m_start - G::HALO;
+  r.st0 = a.state0 + (long long)r.s * a.ns;
+  r.st1 = NCH == 2 ? a.state1 + (long long)r.s * a.ns : nullptr;
+  r.x0 = r.x1 = nullptr;
+  r.iq = nullptr;
+  if constexpr (SRC == Src::F32) {
+    r.x0 = a.x0 + (long long)r.s * a.x_stride;
+    if (NCH == 2) r.x1 = a.x1 + (long long)r.s * a.x_stride;
+  } else {
+    r.iq = a.iq + (long long)r.s * a.x_stride;
+  }
+  return r;
+}
+
+// Issue every global load of one tile span into registers (16-B f32 / 8-B
+// u8 vectors for chunks inside the block; four guarded scalars for the few
+// chunks straddling its start -- old state -- or end -- zeros that never
+// reach a stored output).  No wait: the registers are consumed by stage_store.
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ __forceinline__ void stage_load(const FirLaunch& a, const TileRef& tr, int tid,
+                                           float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                           float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  const long long n = a.n;
+  const int ns = a.ns;
+  auto load4 = [&](int i, float4& a0, float4& a1) {
+    const long long p = tr.pb + 4LL * i;
+    if (p >= 0 && p + 4 <= n) {
+      if constexpr (SRC == Src::F32) {
+        a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
+        if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
+      } else {
+        const uint2 b = *reinterpret_cast<const uint2*>(tr.iq + 2 * p);
+        a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
+                         u8_to_f32((b.y >> 16) & 0xffu));
+        a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
+                         u8_to_f32(b.y >> 24));
+      }
+    } else {
+      a0 = make_float4(edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p),
+                       edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p + 1),
+                       edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p + 2),
+                       edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p + 3));
+      if (NCH == 2)
+        a1 = make_float4(edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p),
+                         edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p + 1),
+                         edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p + 2),
+                         edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p + 3));
+    }
+  };
+#pragma unroll
+  for (int it = 0; it < G::FULL; ++it) load4(tid + it * G::NTH, v0[it], v1[it]);
+  // ragged last row: clamp the index (a redundant load) so every register
+  // is defined and the arrays stay in VGPRs
+  if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
+}
+
+template <int D, int T, int R, bool DEMOD, int NW, int NCH>
+__device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
+                                            const float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                            const float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+#pragma unroll
+  for (int it = 0; it < G::FULL; ++it) {
+    const int i = tid + it * G::NTH;
+    *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[it];
+    if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[it];
+  }
+  if (G::REM && tid < G::REM) {
+    const int i = tid + G::FULL * G::NTH;
+    *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[G::FULL];
+    if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[G::FULL];
+  }
+}
+
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
   using G = Geom<D, T, R, DEMOD, NW>;
@@ -111,251 +204,198 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  // XCD-aware order: blocks b and b+8 share an XCD (round-robin dispatch),
-  // so give each XCD a contiguous run of tiles -- neighbouring tiles of a
-  // stream then re-read each other's halo from the same L2.  Speed only.
-  const unsigned nb = gridDim.x, b = blockIdx.x;
-  const unsigned lin = (nb % 8u == 0u) ? (b % 8u) * (nb / 8u) + b / 8u : b;
-  const int s = (int)(lin / (unsigned)a.tiles_per_stream);
-  const int t = (int)(lin - (unsigned)s * (unsigned)a.tiles_per_stream);
   const long long n = a.n;
   const long long nout = n / D;
-  const long long m_start = (long long)t * G::ADV - G::E;     // first output computed by the tile
-  const long long pb = (long long)D * m_start - G::HALO;      // stream position of LDS index 0
   const int ns = a.ns;
-  float* st0 = a.state0 + (long long)s * ns;
-  float* st1 = NCH == 2 ? a.state1 + (long long)s * ns : nullptr;
-  const float* x0 = nullptr;
-  const float* x1 = nullptr;
-  const uint8_t* iq = nullptr;
-  if constexpr (SRC == Src::F32) {
-    x0 = a.x0 + (long long)s * a.x_stride;
-    if (NCH == 2) x1 = a.x1 + (long long)s * a.x_stride;
-  } else {
-    iq = a.iq + (long long)s * a.x_stride;
-  }
+  const int total = a.nstreams * a.tiles_per_stream;
+  const int first = blockIdx.x * a.tiles_per_wg;
+  const int last = min(first + a.tiles_per_wg, total);
+  if (first >= last) return;
 
-  // ---- 1. stage: tap rows, tile span, and (tile 0) everything the state
-  // carry needs.  Every read of the OLD state / prev happens here, before
-  // the only barrier; tile 0 is the only workgroup that reads them and the
-  // only one that rewrites them (step 4), so no second kernel is needed.
-  float old_pi = 0.0f, old_pq = 0.0f;
-  if constexpr (DEMOD) {
-    if (t == 0 && tid == 1) {
-      old_pi = a.prev0[s];
-      old_pq = a.prev1[s];
-    }
-  }
-  // tap rows: htab[r][w] = h[HALO + D*r - w] (0 where that k is not a tap)
+  // tap rows, once per workgroup: htab[r][w] = h[HALO + D*r - w] (0 where
+  // that k is not a tap)
   for (int i = tid; i < R * G::SPAN4; i += NTH) {
     const int r = i / G::SPAN4, w = i - r * G::SPAN4;
     const int k = G::HALO + D * r - w;
     htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
   }
-  if constexpr (DEMOD) {
-    if (t == 0) {
-      // the T inputs of the block's last decimated sample (prev_* source);
-      // D*(nout-1) - k >= -(T-1) >= -ns, so the old state covers p < 0
-      const long long P = (long long)D * (nout - 1);
-      for (int k = tid; k < T; k += NTH) {
-        const long long p = P - k;
-        tail0[k] = p < 0 ? st0[ns + p] : in_at<SRC>(x0, iq, 0, p);
-        tail1[k] = p < 0 ? st1[ns + p] : in_at<SRC>(x1, iq, 1, p);
-      }
-    }
-  }
-  {
-    // 16-B (f32) / 8-B (u8) coalesced vector loads for every chunk inside
-    // the block; the few chunks that straddle its start (old state) or end
-    // (zeros, never reaching a stored output) take four guarded scalar
-    // loads instead.  Every load is issued before the first LDS store.
-    constexpr int FULL = G::LDS4 / NTH, REM = G::LDS4 % NTH;
-    float4 v0[FULL + 1], v1[FULL + 1];
-    auto load4 = [&](int i, float4& a0, float4& a1) {
-      const long long p = pb + 4LL * i;
-      if (p >= 0 && p + 4 <= n) {
-        if constexpr (SRC == Src::F32) {
-          a0 = *reinterpret_cast<const float4*>(x0 + p);
-          if (NCH == 2) a1 = *reinterpret_cast<const float4*>(x1 + p);
-        } else {
-          const uint2 b = *reinterpret_cast<const uint2*>(iq + 2 * p);
-          a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
-                           u8_to_f32((b.y >> 16) & 0xffu));
-          a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
-                           u8_to_f32(b.y >> 24));
-        }
-      } else {
-        a0 = make_float4(edge_at<SRC>(x0, iq, 0, st0, ns, n, p), edge_at<SRC>(x0, iq, 0, st0, ns, n, p + 1),
-                         edge_at<SRC>(x0, iq, 0, st0, ns, n, p + 2), edge_at<SRC>(x0, iq, 0, st0, ns, n, p + 3));
-        if (NCH == 2)
-          a1 = make_float4(edge_at<SRC>(x1, iq, 1, st1, ns, n, p), edge_at<SRC>(x1, iq, 1, st1, ns, n, p + 1),
-                           edge_at<SRC>(x1, iq, 1, st1, ns, n, p + 2), edge_at<SRC>(x1, iq, 1, st1, ns, n, p + 3));
-      }
-    };
-#pragma unroll
-    for (int it = 0; it < FULL; ++it) load4(tid + it * NTH, v0[it], v1[it]);
-    // the ragged last row: clamp the index (a redundant load) so every
-    // register is defined and the arrays stay in VGPRs
-    const int il = tid < REM ? tid + FULL * NTH : FULL * NTH - 1;
-    if (REM) load4(il, v0[FULL], v1[FULL]);
-#pragma unroll
-    for (int it = 0; it < FULL; ++it) {
-      const int i = tid + it * NTH;
-      *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[it];
-      if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[it];
-    }
-    if (REM && tid < REM) {
-      *reinterpret_cast<float4*>(lds0 + 4 * il) = v0[FULL];
-      if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * il) = v1[FULL];
-    }
-  }
-  __syncthreads();
 
-  // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
-  // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
-  // 4-position chunk c it reads NCH input float4s (its own window; lane
-  // stride D*R dwords, e.g. 20 for D=10: conflict-free ds_read_b128) and R
-  // tap float4s (one address for the whole wave: an LDS broadcast) from
-  // tap rows laid out so that row r, chunk c holds the taps output r applies
-  // to window positions 4c..4c+3.  The next chunk is prefetched; the
-  // sched_barrier keeps the scheduler from hoisting every LDS read of the
-  // unrolled loop (register pressure -> occupancy).
-  const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
-  float acc0[R], acc1[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    acc0[r] = 0.0f;
-    acc1[r] = 0.0f;
-  }
-  {
-    const float* w0 = lds0 + lbase;
-    const float* w1 = lds1 + lbase;
-    constexpr int C0 = G::NCHUNK - 1;
-    float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
-    float4 q1 = q0;
-    if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
-    float4 hq[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) hq[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * C0);
-#pragma unroll
-    for (int c = C0; c >= 0; --c) {
-      float4 n0 = q0, n1 = q1, nh[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) nh[r] = hq[r];
-      if (c > 0) {
-        n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
-        if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
-#pragma unroll
-        for (int r = 0; r < R; ++r) nh[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * (c - 1));
-      }
-      const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
-      const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-      for (int j = 3; j >= 0; --j) {
-        const int w = 4 * c + j;  // window position; output r sits at HALO + D*r
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int k = G::HALO + D * r - w;
-          if (k >= 0 && k < T) {
-            const float hk = j == 0 ? hq[r].x : j == 1 ? hq[r].y : j == 2 ? hq[r].z : hq[r].w;
-            acc0[r] = acc0[r] + hk * e0[j];
-            if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
-          }
+  float4 v0[G::FULL + 1], v1[G::FULL + 1];
+  stage_load<D, T, R, DEMOD, NW, NCH, SRC>(a, tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), tid, v0, v1);
+
+  for (int lin = first; lin < last; ++lin) {
+    const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
+
+    // Old prev_I/prev_Q and the T inputs of the block's last decimated
+    // sample (the prev_* carry source), read before this workgroup rewrites
+    // state/prev at the end of the iteration.  D*(nout-1) - k >= -(T-1) >=
+    // -ns, so the old state covers p < 0.
+    float old_pi = 0.0f, old_pq = 0.0f;
+    if constexpr (DEMOD) {
+      if (tr.t == 0) {
+        if (tid == 1) {
+          old_pi = a.prev0[tr.s];
+          old_pq = a.prev1[tr.s];
+        }
+        const long long P = (long long)D * (nout - 1);
+        for (int k = tid; k < T; k += NTH) {
+          const long long p = P - k;
+          tail0[k] = p < 0 ? tr.st0[ns + p] : in_at<SRC>(tr.x0, tr.iq, 0, p);
+          tail1[k] = p < 0 ? tr.st1[ns + p] : in_at<SRC>(tr.x1, tr.iq, 1, p);
         }
       }
-      q0 = n0;
-      q1 = n1;
-#pragma unroll
-      for (int r = 0; r < R; ++r) hq[r] = nh[r];
-      // Pin both channels' chains to this chunk: without it LLVM defers
-      // one channel's products past later chunks (holding their operands
-      // live -> 256 VGPRs at R = 4).
-#pragma unroll
-      for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
-      __builtin_amdgcn_sched_barrier(0);
     }
-  }
 
-  const long long m0 = m_start + (long long)wave * G::WADV + (long long)R * lane;  // first output of this lane
-  if constexpr (DEMOD) {
-    // ---- 3. discriminator in registers.  The decimated sample before
-    // output r=0 is lane-1's last output (a wave shuffle); lane 0's outputs
-    // are the wave's overlap and are not stored; at the start of the
-    // stream (tile 0, wave 0, lane 1 -> output 0) it is the carried prev_*.
-    float pI = __shfl_up(acc0[R - 1], 1, 64);
-    float pQ = __shfl_up(acc1[R - 1], 1, 64);
-    if (t == 0 && tid == 1) {
-      pI = old_pi;
-      pQ = old_pq;
-    }
-    float d[R];
+    // ---- 1. registers -> LDS (after every read of the previous tile), then
+    // prefetch the next tile into the registers just freed
+    __syncthreads();
+    stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    __syncthreads();
+    if (lin + 1 < last)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(a, tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), tid, v0, v1);
+
+    // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
+    // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
+    // 4-position chunk c it reads NCH input float4s (its own window) and R
+    // tap float4s (one address for the whole wave: an LDS broadcast); the
+    // next chunk is prefetched; the sched_barrier keeps the scheduler from
+    // hoisting every LDS read of the unrolled loop (registers -> occupancy).
+    const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
+    float acc0[R], acc1[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const float ip = r ? acc0[r - 1] : pI;
-      const float qp = r ? acc1[r - 1] : pQ;
-      d[r] = demod_one(acc0[r], acc1[r], ip, qp);
+      acc0[r] = 0.0f;
+      acc1[r] = 0.0f;
     }
-    float* o = a.out + (long long)s * a.out_stride;
-    // vector stores when this stream's row keeps R-float groups aligned
-    // (uniform per workgroup); scalar stores otherwise
-    const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)m_start) % (4u * R)) == 0;
-    if (lane >= 1) {
-      if (vec && m0 + R <= nout) {
-        if constexpr (R == 2) {
-          *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);
-        } else if constexpr (R == 4) {
-          *reinterpret_cast<float4*>(o + m0) = make_float4(d[0], d[1], d[2], d[3]);
+    {
+      const float* w0 = lds0 + lbase;
+      const float* w1 = lds1 + lbase;
+      constexpr int C0 = G::NCHUNK - 1;
+      float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
+      float4 q1 = q0;
+      if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
+      float4 hq[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) hq[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * C0);
+#pragma unroll
+      for (int c = C0; c >= 0; --c) {
+        float4 n0 = q0, n1 = q1, nh[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) nh[r] = hq[r];
+        if (c > 0) {
+          n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
+          if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+#pragma unroll
+          for (int r = 0; r < R; ++r) nh[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * (c - 1));
+        }
+        const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+        const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          const int w = 4 * c + j;  // window position; output r sits at HALO + D*r
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int k = G::HALO + D * r - w;
+            if (k >= 0 && k < T) {
+              const float hk = j == 0 ? hq[r].x : j == 1 ? hq[r].y : j == 2 ? hq[r].z : hq[r].w;
+              acc0[r] = acc0[r] + hk * e0[j];
+              if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
+            }
+          }
+        }
+        q0 = n0;
+        q1 = n1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) hq[r] = nh[r];
+        // Pin both channels' chains to this chunk: without it LLVM defers
+        // one channel's products past later chunks (holding their operands
+        // live -> 256 VGPRs at R = 4).
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    const long long m0 = tr.m_start + (long long)wave * G::WADV + (long long)R * lane;  // this lane's first output
+    if constexpr (DEMOD) {
+      // ---- 3. discriminator in registers.  The decimated sample before
+      // output r=0 is lane-1's last output (a wave shuffle); lane 0's
+      // outputs are the wave's overlap and are not stored; at the start of
+      // the stream (tile 0, wave 0, lane 1 -> output 0) it is the carried prev_*.
+      float pI = __shfl_up(acc0[R - 1], 1, 64);
+      float pQ = __shfl_up(acc1[R - 1], 1, 64);
+      if (tr.t == 0 && tid == 1) {
+        pI = old_pi;
+        pQ = old_pq;
+      }
+      float d[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float ip = r ? acc0[r - 1] : pI;
+        const float qp = r ? acc1[r - 1] : pQ;
+        d[r] = demod_one(acc0[r], acc1[r], ip, qp);
+      }
+      float* o = a.out + (long long)tr.s * a.out_stride;
+      // vector stores when the row keeps R-float groups aligned (uniform)
+      const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+      if (lane >= 1) {
+        if (vec && m0 + R <= nout) {
+          if constexpr (R == 2) {
+            *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);
+          } else if constexpr (R == 4) {
+            *reinterpret_cast<float4*>(o + m0) = make_float4(d[0], d[1], d[2], d[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
+          }
         } else {
 #pragma unroll
-          for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
+          for (int r = 0; r < R; ++r)
+            if (m0 + r < nout) o[m0 + r] = d[r];
+        }
+      }
+    } else {
+      float* o = a.y0 + (long long)tr.s * a.y_stride;
+      const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+      if (vec && m0 + R <= nout) {
+        if constexpr (R == 4) {
+          *reinterpret_cast<float4*>(o + m0) = make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
+        } else if constexpr (R == 2) {
+          *reinterpret_cast<float2*>(o + m0) = make_float2(acc0[0], acc0[1]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) o[m0 + r] = acc0[r];
         }
       } else {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-          if (m0 + r < nout) o[m0 + r] = d[r];
+          if (m0 + r < nout) o[m0 + r] = acc0[r];
       }
     }
-  } else {
-    float* o = a.y0 + (long long)s * a.y_stride;
-    const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)m_start) % (4u * R)) == 0;
-    if (vec && m0 + R <= nout) {
-      if constexpr (R == 4) {
-        *reinterpret_cast<float4*>(o + m0) = make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
-      } else if constexpr (R == 2) {
-        *reinterpret_cast<float2*>(o + m0) = make_float2(acc0[0], acc0[1]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r) o[m0 + r] = acc0[r];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (m0 + r < nout) o[m0 + r] = acc0[r];
-    }
-  }
 
-  // ---- 4. state carry (tile 0 only; its reads of the old values all
-  // happened before the barrier above)
-  if (t == 0) {
-    if constexpr (DEMOD) {
-      // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
-      // recomputed in the reference's order from the staged strip
-      if (tid == 0) {
-        float yi = 0.0f, yq = 0.0f;
-        for (int k = 0; k < T; ++k) {
-          const float hk = h[k];
-          yi = yi + hk * tail0[k];
-          yq = yq + hk * tail1[k];
+    // ---- 4. state carry (tile 0 only; every read of the old values
+    // happened before the barriers above)
+    if (tr.t == 0) {
+      if constexpr (DEMOD) {
+        // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
+        // recomputed in the reference's order from the staged strip
+        if (tid == 0) {
+          float yi = 0.0f, yq = 0.0f;
+          for (int k = 0; k < T; ++k) {
+            const float hk = h[k];
+            yi = yi + hk * tail0[k];
+            yq = yq + hk * tail1[k];
+          }
+          a.prev0[tr.s] = yi;
+          a.prev1[tr.s] = yq;
         }
-        a.prev0[s] = yi;
-        a.prev1[s] = yq;
       }
-    }
-    // state <- last ns input samples (src/filter.cpp:139)
-    for (int j = tid; j < ns; j += NTH) {
-      const long long p = n - ns + j;
-      st0[j] = in_at<SRC>(x0, iq, 0, p);
-      if (NCH == 2) st1[j] = in_at<SRC>(x1, iq, 1, p);
+      // state <- last ns input samples (src/filter.cpp:139)
+      for (int j = tid; j < ns; j += NTH) {
+        const long long p = n - ns + j;
+        tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, p);
+        if (NCH == 2) tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
+      }
     }
   }
 }
@@ -431,17 +471,33 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 }
 
 // ------------------------------------------------------------ dispatch ----
+// Persistent grid: about `waves_per_cu` single-wave workgroups per CU (or the
+// tile count, if smaller), each walking a contiguous run of tiles.
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
   const long long nout = a.n / D;
   a.tiles_per_stream = (int)((nout + G::ADV - 1) / G::ADV);
+  const long long total = (long long)a.tiles_per_stream * a.nstreams;
+  if (total <= 0 || total > 0x7fffffffLL) return hipErrorInvalidValue;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  static const int per_cu = [] {
+    const char* e = std::getenv("SDR_WG_PER_CU");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 12;
+  }();
+  const long long slots = (long long)ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
+  const long long grid = total < slots ? total : slots;
+  a.tiles_per_wg = (int)((total + grid - 1) / grid);
+  const long long blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
   const size_t lds = (size_t)G::SMEM * sizeof(float);
-  const long long blocks = (long long)a.tiles_per_stream * a.nstreams;
-  if (blocks <= 0 || blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a,
-                     h);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();
 }
 

@@ -41,6 +41,7 @@ struct FirLaunch {
   float* out;
   long long out_stride;
   int tiles_per_stream;
+  int tiles_per_wg;  // persistent tile kernels: contiguous tiles per workgroup
 };
 
 // Exact reference conversion of one wire byte, src/iofunc.cpp:118:
