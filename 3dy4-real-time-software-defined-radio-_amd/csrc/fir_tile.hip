@@ -127,40 +127,30 @@ __device__ __forceinline__ TileRef tile_ref(const FirLaunch& a, int lin) {
   return r;
 }
 
-// Issue every global load of one tile span into registers (16-B f32 / 8-B
-// u8 vectors for chunks inside the block; four guarded scalars for the few
-// chunks straddling its start -- old state -- or end -- zeros that never
-// reach a stored output).  No wait: the registers are consumed by stage_store.
+// A tile whose whole span lies inside the block: no state, no tail.
+template <int D, int T, int R, bool DEMOD, int NW>
+__device__ __forceinline__ bool interior(const TileRef& tr, long long n) {
+  return tr.pb >= 0 && tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n;
+}
+
+// Issue every global load of an interior tile span into registers (16-B
+// f32 / 8-B u8 coalesced vectors).  No wait: stage_store consumes them.
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
-__device__ __forceinline__ void stage_load(const FirLaunch& a, const TileRef& tr, int tid,
+__device__ __forceinline__ void stage_load(const TileRef& tr, int tid,
                                            float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
                                            float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   using G = Geom<D, T, R, DEMOD, NW>;
-  const long long n = a.n;
-  const int ns = a.ns;
   auto load4 = [&](int i, float4& a0, float4& a1) {
     const long long p = tr.pb + 4LL * i;
-    if (p >= 0 && p + 4 <= n) {
-      if constexpr (SRC == Src::F32) {
-        a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
-        if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
-      } else {
-        const uint2 b = *reinterpret_cast<const uint2*>(tr.iq + 2 * p);
-        a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
-                         u8_to_f32((b.y >> 16) & 0xffu));
-        a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
-                         u8_to_f32(b.y >> 24));
-      }
+    if constexpr (SRC == Src::F32) {
+      a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
+      if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
     } else {
-      a0 = make_float4(edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p),
-                       edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p + 1),
-                       edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p + 2),
-                       edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p + 3));
-      if (NCH == 2)
-        a1 = make_float4(edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p),
-                         edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p + 1),
-                         edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p + 2),
-                         edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p + 3));
+      const uint2 b = *reinterpret_cast<const uint2*>(tr.iq + 2 * p);
+      a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
+                       u8_to_f32((b.y >> 16) & 0xffu));
+      a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
+                       u8_to_f32(b.y >> 24));
     }
   };
 #pragma unroll
@@ -168,6 +158,19 @@ __device__ __forceinline__ void stage_load(const FirLaunch& a, const TileRef& tr
   // ragged last row: clamp the index (a redundant load) so every register
   // is defined and the arrays stay in VGPRs
   if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
+}
+
+// First / last tile of a stream (about 2 in every tiles_per_stream): fill
+// LDS directly, element-wise, with the old state before the block and zeros
+// past its end (zeros never reach a stored output).
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ void fill_edge(const TileRef& tr, int tid, long long n, int ns, float* lds0, float* lds1) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  for (int i = tid; i < G::LDS_LEN; i += G::NTH) {
+    const long long p = tr.pb + i;
+    lds0[i] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+    if (NCH == 2) lds1[i] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+  }
 }
 
 template <int D, int T, int R, bool DEMOD, int NW, int NCH>
@@ -221,7 +224,12 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   }
 
   float4 v0[G::FULL + 1], v1[G::FULL + 1];
-  stage_load<D, T, R, DEMOD, NW, NCH, SRC>(a, tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), tid, v0, v1);
+#pragma unroll
+  for (int i = 0; i <= G::FULL; ++i) v0[i] = v1[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // keeps them in VGPRs
+  {
+    const TileRef t0 = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first);
+    if (interior<D, T, R, DEMOD, NW>(t0, n)) stage_load<D, T, R, DEMOD, NW, NCH, SRC>(t0, tid, v0, v1);
+  }
 
   for (int lin = first; lin < last; ++lin) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
@@ -249,17 +257,26 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // ---- 1. registers -> LDS (after every read of the previous tile), then
     // prefetch the next tile into the registers just freed
     __syncthreads();
-    stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    if (interior<D, T, R, DEMOD, NW>(tr, n))  // workgroup-uniform
+      stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    else
+      fill_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
     __syncthreads();
-    if (lin + 1 < last)
-      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(a, tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), tid, v0, v1);
+    if (lin + 1 < last) {
+      const TileRef tn = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1);
+      if (interior<D, T, R, DEMOD, NW>(tn, n)) stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tn, tid, v0, v1);
+    }
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
-    // 4-position chunk c it reads NCH input float4s (its own window) and R
-    // tap float4s (one address for the whole wave: an LDS broadcast); the
-    // next chunk is prefetched; the sched_barrier keeps the scheduler from
-    // hoisting every LDS read of the unrolled loop (registers -> occupancy).
+    // 4-position chunk c it reads NCH input float4s from its own LDS window
+    // (prefetched one chunk ahead).  Tap k is a compile-time index, so the
+    // taps are SGPR operands of the multiplies, fetched by scalar loads chunk
+    // by chunk: the tap pointer is laundered per tile (no hoisting out of the
+    // tile loop) and the sched_barrier keeps each chunk's loads in place --
+    // otherwise all 101 taps are hoisted into SGPRs and spill.
+    const float* hs;
+    asm volatile("" : "=s"(hs) : "0"(h));
     const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
     float acc0[R], acc1[R];
 #pragma unroll
@@ -274,19 +291,12 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
       float4 q1 = q0;
       if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
-      float4 hq[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) hq[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * C0);
 #pragma unroll
       for (int c = C0; c >= 0; --c) {
-        float4 n0 = q0, n1 = q1, nh[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) nh[r] = hq[r];
+        float4 n0 = q0, n1 = q1;
         if (c > 0) {
           n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
           if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
-#pragma unroll
-          for (int r = 0; r < R; ++r) nh[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * (c - 1));
         }
         const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
         const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
@@ -297,7 +307,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           for (int r = 0; r < R; ++r) {
             const int k = G::HALO + D * r - w;
             if (k >= 0 && k < T) {
-              const float hk = j == 0 ? hq[r].x : j == 1 ? hq[r].y : j == 2 ? hq[r].z : hq[r].w;
+              const float hk = hs[k];
               acc0[r] = acc0[r] + hk * e0[j];
               if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
             }
@@ -305,8 +315,6 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
         }
         q0 = n0;
         q1 = n1;
-#pragma unroll
-        for (int r = 0; r < R; ++r) hq[r] = nh[r];
         // Pin both channels' chains to this chunk: without it LLVM defers
         // one channel's products past later chunks (holding their operands
         // live -> 256 VGPRs at R = 4).
