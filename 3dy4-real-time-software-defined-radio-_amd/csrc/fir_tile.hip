@@ -133,15 +133,18 @@ __device__ __forceinline__ bool interior(const TileRef& tr, long long n) {
   return tr.pb >= 0 && tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n;
 }
 
-// Issue every global load of an interior tile span into registers (16-B
-// f32 / 8-B u8 coalesced vectors).  No wait: stage_store consumes them.
+// Issue every global load of one tile span into registers (16-B f32 / 8-B
+// u8 coalesced vectors).  Chunk addresses are clamped into the block, so an
+// edge tile loads in-bounds but partly wrong data that fix_edge() then
+// overwrites.  No wait: stage_store consumes the registers.
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
-__device__ __forceinline__ void stage_load(const TileRef& tr, int tid,
+__device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int tid,
                                            float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
                                            float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   using G = Geom<D, T, R, DEMOD, NW>;
   auto load4 = [&](int i, float4& a0, float4& a1) {
-    const long long p = tr.pb + 4LL * i;
+    long long p = tr.pb + 4LL * i;
+    p = p < 0 ? 0 : (p > n - 4 ? n - 4 : p);
     if constexpr (SRC == Src::F32) {
       a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
       if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
@@ -160,16 +163,23 @@ __device__ __forceinline__ void stage_load(const TileRef& tr, int tid,
   if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
 }
 
-// First / last tile of a stream (about 2 in every tiles_per_stream): fill
-// LDS directly, element-wise, with the old state before the block and zeros
-// past its end (zeros never reach a stored output).
+// First / last tile of a stream (about 2 in every tiles_per_stream): after
+// the clamped vector fill, rewrite the span elements whose chunk was clamped
+// -- the old state before the block, the true samples of the chunk
+// straddling its end (n need not be a multiple of 4), zeros past it (they
+// never reach a stored output).  The tile span starts 16-B aligned, so no
+// chunk straddles position 0.
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
-__device__ void fill_edge(const TileRef& tr, int tid, long long n, int ns, float* lds0, float* lds1) {
+__device__ __forceinline__ void fix_edge(const TileRef& tr, int tid, long long n, int ns, float* lds0,
+                                         float* lds1) {
   using G = Geom<D, T, R, DEMOD, NW>;
+  const long long tail_from = (n - 4) & ~3LL;  // no clamped chunk starts below min(n-4 rounded, ...)
   for (int i = tid; i < G::LDS_LEN; i += G::NTH) {
     const long long p = tr.pb + i;
-    lds0[i] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
-    if (NCH == 2) lds1[i] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+    if (p < 0 || p >= tail_from) {
+      lds0[i] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+      if (NCH == 2) lds1[i] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+    }
   }
 }
 
@@ -226,10 +236,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   float4 v0[G::FULL + 1], v1[G::FULL + 1];
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) v0[i] = v1[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // keeps them in VGPRs
-  {
-    const TileRef t0 = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first);
-    if (interior<D, T, R, DEMOD, NW>(t0, n)) stage_load<D, T, R, DEMOD, NW, NCH, SRC>(t0, tid, v0, v1);
-  }
+  stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, v0, v1);
 
   for (int lin = first; lin < last; ++lin) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
@@ -257,15 +264,14 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // ---- 1. registers -> LDS (after every read of the previous tile), then
     // prefetch the next tile into the registers just freed
     __syncthreads();
-    if (interior<D, T, R, DEMOD, NW>(tr, n))  // workgroup-uniform
-      stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
-    else
-      fill_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
-    __syncthreads();
-    if (lin + 1 < last) {
-      const TileRef tn = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1);
-      if (interior<D, T, R, DEMOD, NW>(tn, n)) stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tn, tid, v0, v1);
+    stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    if (!interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
+      __syncthreads();
+      fix_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
     }
+    __syncthreads();
+    if (lin + 1 < last)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), n, tid, v0, v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
