@@ -275,14 +275,10 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
-    // 4-position chunk c it reads NCH input float4s from its own LDS window
-    // (prefetched one chunk ahead).  Tap k is a compile-time index, so the
-    // taps are SGPR operands of the multiplies, fetched by scalar loads chunk
-    // by chunk: the tap pointer is laundered per tile (no hoisting out of the
-    // tile loop) and the sched_barrier keeps each chunk's loads in place --
-    // otherwise all 101 taps are hoisted into SGPRs and spill.
-    const float* hs;
-    asm volatile("" : "=s"(hs) : "0"(h));
+    // 4-position chunk c it reads NCH input float4s (its own window) and R
+    // tap float4s (one address for the whole wave: an LDS broadcast); the
+    // next chunk is prefetched; the sched_barrier keeps the scheduler from
+    // hoisting every LDS read of the unrolled loop (registers -> occupancy).
     const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
     float acc0[R], acc1[R];
 #pragma unroll
@@ -297,12 +293,19 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
       float4 q1 = q0;
       if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
+      float4 hq[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) hq[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * C0);
 #pragma unroll
       for (int c = C0; c >= 0; --c) {
-        float4 n0 = q0, n1 = q1;
+        float4 n0 = q0, n1 = q1, nh[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) nh[r] = hq[r];
         if (c > 0) {
           n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
           if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+#pragma unroll
+          for (int r = 0; r < R; ++r) nh[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * (c - 1));
         }
         const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
         const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           for (int r = 0; r < R; ++r) {
             const int k = G::HALO + D * r - w;
             if (k >= 0 && k < T) {
-              const float hk = hs[k];
+              const float hk = j == 0 ? hq[r].x : j == 1 ? hq[r].y : j == 2 ? hq[r].z : hq[r].w;
               acc0[r] = acc0[r] + hk * e0[j];
               if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
             }
@@ -321,6 +324,8 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
         }
         q0 = n0;
         q1 = n1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) hq[r] = nh[r];
         // Pin both channels' chains to this chunk: without it LLVM defers
         // one channel's products past later chunks (holding their operands
         // live -> 256 VGPRs at R = 4).
