@@ -49,6 +49,10 @@ struct Geom {
   static constexpr int SPAN = HALO + D * (R - 1) + 1;              // positions one lane reads
   static constexpr int NCHUNK = (SPAN + 3) / 4;                    // float4 chunks per lane window
   static constexpr int SPAN4 = 4 * NCHUNK;                         // tap row length
+  // tap-row reuse: rows GR apart are offset by D*GR taps = SH whole chunks
+  static constexpr int GQ = (D % 4 == 0) ? 1 : (D % 2 == 0) ? 2 : 4;
+  static constexpr int GR = GQ < R ? GQ : R;                       // tap rows read from LDS per chunk
+  static constexpr int SH = D * GR / 4;                            // chunk shift between reused rows
   static constexpr int LDS_LEN = D * ((NW - 1) * WADV + 63 * R) + SPAN4;  // floats per channel
   static constexpr int LDS4 = LDS_LEN / 4;
   static constexpr int FULL = LDS4 / NTH, REM = LDS4 % NTH;        // staging rows per thread
@@ -275,10 +279,15 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
-    // 4-position chunk c it reads NCH input float4s (its own window) and R
-    // tap float4s (one address for the whole wave: an LDS broadcast); the
-    // next chunk is prefetched; the sched_barrier keeps the scheduler from
-    // hoisting every LDS read of the unrolled loop (registers -> occupancy).
+    // 4-position chunk c it reads NCH input float4s (its own window) and the
+    // taps of the top GR output rows (one address for the whole wave: an LDS
+    // broadcast).  Output row r < R-GR applies, at chunk c, exactly the taps
+    // row r+GR applied at chunk c+SH (D*GR is a multiple of 4), so those
+    // come from registers loaded SH chunks earlier: at R = 4, D = 10 half
+    // the tap reads disappear.  The next chunk is prefetched; the
+    // sched_barrier keeps the scheduler from hoisting every LDS read of the
+    // unrolled loop (registers -> occupancy).
+    constexpr int GR = G::GR, SH = G::SH, C0 = G::NCHUNK - 1;
     const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
     float acc0[R], acc1[R];
 #pragma unroll
@@ -289,23 +298,22 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
-      constexpr int C0 = G::NCHUNK - 1;
+      const float* ht = htab + (R - GR) * G::SPAN4;  // the top GR rows
+      float4 top[G::NCHUNK][GR];                     // compile-time indexed: SSA values
       float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
       float4 q1 = q0;
       if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
-      float4 hq[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) hq[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * C0);
+      for (int g = 0; g < GR; ++g) top[C0][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * C0);
 #pragma unroll
       for (int c = C0; c >= 0; --c) {
-        float4 n0 = q0, n1 = q1, nh[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) nh[r] = hq[r];
+        float4 n0 = q0, n1 = q1;
         if (c > 0) {
           n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
           if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
 #pragma unroll
-          for (int r = 0; r < R; ++r) nh[r] = *reinterpret_cast<const float4*>(htab + r * G::SPAN4 + 4 * (c - 1));
+          for (int g = 0; g < GR; ++g)
+            top[c - 1][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * (c - 1));
         }
         const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
         const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
@@ -316,7 +324,10 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           for (int r = 0; r < R; ++r) {
             const int k = G::HALO + D * r - w;
             if (k >= 0 && k < T) {
-              const float hk = j == 0 ? hq[r].x : j == 1 ? hq[r].y : j == 2 ? hq[r].z : hq[r].w;
+              // row r at chunk c == top row r + m*GR at chunk c + m*SH
+              const int m = r >= R - GR ? 0 : (R - GR - r + GR - 1) / GR;
+              const float4 hv = top[c + m * SH][r + m * GR - (R - GR)];
+              const float hk = j == 0 ? hv.x : j == 1 ? hv.y : j == 2 ? hv.z : hv.w;
               acc0[r] = acc0[r] + hk * e0[j];
               if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
             }
@@ -324,8 +335,6 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
         }
         q0 = n0;
         q1 = n1;
-#pragma unroll
-        for (int r = 0; r < R; ++r) hq[r] = nh[r];
         // Pin both channels' chains to this chunk: without it LLVM defers
         // one channel's products past later chunks (holding their operands
         // live -> 256 VGPRs at R = 4).
