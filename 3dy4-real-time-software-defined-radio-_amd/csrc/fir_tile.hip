@@ -240,7 +240,8 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   float4 v0[G::FULL + 1], v1[G::FULL + 1];
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) v0[i] = v1[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // keeps them in VGPRs
-  stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, v0, v1);
+  if (a.ablate != 1)
+    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, v0, v1);
 
   for (int lin = first; lin < last; ++lin) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       fix_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
     }
     __syncthreads();
-    if (lin + 1 < last)
+    if (lin + 1 < last && a.ablate != 1)
       stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), n, tid, v0, v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
@@ -295,7 +296,10 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       acc0[r] = 0.0f;
       acc1[r] = 0.0f;
     }
-    {
+    if (a.ablate == 2) {
+      acc0[0] = lds0[lbase];
+      acc1[0] = lds1[lbase];
+    } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
       const float* ht = htab + (R - GR) * G::SPAN4;  // the top GR rows
@@ -524,6 +528,11 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   const long long grid = total < slots ? total : slots;
   a.tiles_per_wg = (int)((total + grid - 1) / grid);
   const long long blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
+  static const int ablate = [] {
+    const char* e = std::getenv("SDR_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.ablate = ablate;
   const size_t lds = (size_t)G::SMEM * sizeof(float);
   hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();

@@ -42,6 +42,7 @@ struct FirLaunch {
   long long out_stride;
   int tiles_per_stream;
   int tiles_per_wg;  // persistent tile kernels: contiguous tiles per workgroup
+  int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math
 };
 
 // Exact reference conversion of one wire byte, src/iofunc.cpp:118:
