@@ -205,8 +205,12 @@ __device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
   }
 }
 
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC>
+// MODE 0: next tile prefetched into registers, taps as LDS broadcast rows.
+// MODE 1: tile filled by LDS-DMA (global_load_lds, f32 only; no staging
+//         registers), taps held in VGPRs -- the scan then reads only x.
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int MODE>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
+  static_assert(MODE == 0 || SRC == Src::F32, "LDS-DMA moves raw f32");
   using G = Geom<D, T, R, DEMOD, NW>;
   constexpr int NTH = G::NTH;
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
@@ -237,11 +241,20 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
   }
 
-  float4 v0[G::FULL + 1], v1[G::FULL + 1];
+  float4 v0[MODE == 0 ? G::FULL + 1 : 1], v1[MODE == 0 ? G::FULL + 1 : 1];
+  float hreg[MODE == 1 ? T : 1];
+  if constexpr (MODE == 0) {
 #pragma unroll
-  for (int i = 0; i <= G::FULL; ++i) v0[i] = v1[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // keeps them in VGPRs
-  if (a.ablate != 1)
-    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, v0, v1);
+    for (int i = 0; i <= G::FULL; ++i) v0[i] = v1[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // keeps them in VGPRs
+    if (a.ablate != 1)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, v0, v1);
+  } else {
+    // taps into VGPRs once (uniform values): row 0 of the tap table holds
+    // h[HALO - w] at w
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < T; ++k) hreg[k] = htab[G::HALO - k];
+  }
 
   for (int lin = first; lin < last; ++lin) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
@@ -269,14 +282,34 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // ---- 1. registers -> LDS (after every read of the previous tile), then
     // prefetch the next tile into the registers just freed
     __syncthreads();
-    stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    if constexpr (MODE == 0) {
+      stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    } else if (a.ablate != 1) {
+      // LDS-DMA: each wave-instruction moves 64 x 16 B = 1 KiB of the span
+      // straight into LDS (linear destination, per-lane source address)
+      typedef __attribute__((address_space(3))) void lds_t;
+      typedef __attribute__((address_space(1))) const void glb_t;
+#pragma unroll
+      for (int it = 0; it <= G::FULL; ++it) {
+        const int i = tid + it * NTH;
+        if (it < G::FULL || tid < G::REM) {
+          long long p = tr.pb + 4LL * i;
+          p = p < 0 ? 0 : (p > n - 4 ? n - 4 : p);
+          __builtin_amdgcn_global_load_lds((glb_t*)(tr.x0 + p), (lds_t*)(lds0 + 4 * (it * NTH)), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((glb_t*)(tr.x1 + p), (lds_t*)(lds1 + 4 * (it * NTH)), 16, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (!interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
       fix_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
     }
     __syncthreads();
-    if (lin + 1 < last && a.ablate != 1)
-      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), n, tid, v0, v1);
+    if constexpr (MODE == 0) {
+      if (lin + 1 < last && a.ablate != 1)
+        stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), n, tid, v0, v1);
+    }
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
@@ -307,17 +340,21 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
       float4 q1 = q0;
       if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
+      if constexpr (MODE == 0) {
 #pragma unroll
-      for (int g = 0; g < GR; ++g) top[C0][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * C0);
+        for (int g = 0; g < GR; ++g) top[C0][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * C0);
+      }
 #pragma unroll
       for (int c = C0; c >= 0; --c) {
         float4 n0 = q0, n1 = q1;
         if (c > 0) {
           n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
           if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+          if constexpr (MODE == 0) {
 #pragma unroll
-          for (int g = 0; g < GR; ++g)
-            top[c - 1][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * (c - 1));
+            for (int g = 0; g < GR; ++g)
+              top[c - 1][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * (c - 1));
+          }
         }
         const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
         const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
@@ -328,10 +365,15 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           for (int r = 0; r < R; ++r) {
             const int k = G::HALO + D * r - w;
             if (k >= 0 && k < T) {
-              // row r at chunk c == top row r + m*GR at chunk c + m*SH
-              const int m = r >= R - GR ? 0 : (R - GR - r + GR - 1) / GR;
-              const float4 hv = top[c + m * SH][r + m * GR - (R - GR)];
-              const float hk = j == 0 ? hv.x : j == 1 ? hv.y : j == 2 ? hv.z : hv.w;
+              float hk;
+              if constexpr (MODE == 1) {
+                hk = hreg[k];
+              } else {
+                // row r at chunk c == top row r + m*GR at chunk c + m*SH
+                const int m = r >= R - GR ? 0 : (R - GR - r + GR - 1) / GR;
+                const float4 hv = top[c + m * SH][r + m * GR - (R - GR)];
+                hk = j == 0 ? hv.x : j == 1 ? hv.y : j == 2 ? hv.z : hv.w;
+              }
               acc0[r] = acc0[r] + hk * e0[j];
               if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
             }
@@ -505,7 +547,7 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 // ------------------------------------------------------------ dispatch ----
 // Persistent grid: about `waves_per_cu` single-wave workgroups per CU (or the
 // tile count, if smaller), each walking a contiguous run of tiles.
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int MODE = 0>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
@@ -522,7 +564,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   static const int per_cu = [] {
     const char* e = std::getenv("SDR_WG_PER_CU");
     const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 12;
+    return v > 0 ? v : 48;
   }();
   const long long slots = (long long)ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
   const long long grid = total < slots ? total : slots;
@@ -534,7 +576,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   }();
   a.ablate = ablate;
   const size_t lds = (size_t)G::SMEM * sizeof(float);
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, MODE>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();
 }
 
@@ -543,15 +585,17 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
 // per D is the measured best on MI355X; SDR_FIR_VARIANT=<R>x<NW>
 // (e.g. "2x1") overrides it for experiments.
 struct Variant {
-  int R, NW;
+  int R, NW, mode;  // mode: 0 register prefetch + LDS tap rows, 1 LDS-DMA + VGPR taps (f32 only)
 };
 
 Variant variant_for(int D, bool demod) {
   static const char* env = std::getenv("SDR_FIR_VARIANT");
   if (env) {
     int r = 0, w = 0;
-    if (std::sscanf(env, "%dx%d", &r, &w) == 2) {
-      const Variant v{r, w};
+    char m = 0;
+    const int got = std::sscanf(env, "%dx%d%c", &r, &w, &m);
+    if (got >= 2) {
+      const Variant v{r, w, m == 'd' ? 1 : 0};
       const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
                          (D == 5 && r == 4 && (w == 1 || w == 4)) ||
                          (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
@@ -559,10 +603,10 @@ Variant variant_for(int D, bool demod) {
     }
   }
   switch (D) {
-    case 10: return {2, 1};
-    case 5: return {4, 1};
-    case 1: return {4, 1};
-    default: return {0, 0};
+    case 10: return {2, 1, 0};
+    case 5: return {4, 1, 0};
+    case 1: return {4, 1, 0};
+    default: return {0, 0, 0};
   }
 }
 
@@ -582,6 +626,15 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
   const Variant v = variant_for(a.D, DEMOD);
   const int key = a.D * 10000 + v.R * 100 + v.NW;
   if (a.ntaps == 101) {
+    if constexpr (SRC == Src::F32) {
+      if (v.mode == 1) {
+        switch (key) {
+          case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st);
+          case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st);
+          default: break;
+        }
+      }
+    }
     switch (key) {
       case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC>(a, h, st);
       case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC>(a, h, st);
