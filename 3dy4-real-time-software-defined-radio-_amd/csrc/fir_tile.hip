@@ -18,7 +18,9 @@
 //   * every lane slides down its own D*R-aligned window of the tile in 16-B
 //     ds_read_b128 chunks (lane stride D*R dwords, 20 for D=10 R=2:
 //     conflict-free) and keeps all R outputs of I and Q in registers; the
-//     taps come from per-output LDS rows read as wave-wide broadcasts;
+//     taps are SGPR operands of the multiplies, loaded once per pass over a
+//     third of the taps (TM 1, default), or per-output LDS rows read as
+//     wave-wide broadcasts (TM 0);
 //   * fused launches apply the discriminator in registers and write only the
 //     demodulated stream: decimated I/Q never touch HBM.  Lane 0 of each wave
 //     re-derives the R outputs before its span (E = R) so waves never wait on
@@ -30,6 +32,7 @@
 //     the workgroup that owns it rewrites them after its reads -- one kernel.
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "sdr_common.hpp"
 
@@ -205,12 +208,20 @@ __device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
   }
 }
 
-// MODE 0: next tile prefetched into registers, taps as LDS broadcast rows.
-// MODE 1: tile filled by LDS-DMA (global_load_lds, f32 only; no staging
-//         registers), taps held in VGPRs -- the scan then reads only x.
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int MODE>
+// f(integral_constant<int, B>), f(<B+1>), ..., f(<E-1>): a fully unrolled
+// loop whose index is a constant expression in the body.
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// TM = where the taps live: 0 LDS broadcast rows, 1 SGPRs (NPASS passes).
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
-  static_assert(MODE == 0 || SRC == Src::F32, "LDS-DMA moves raw f32");
+  constexpr int PF = 1;
   using G = Geom<D, T, R, DEMOD, NW>;
   constexpr int NTH = G::NTH;
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
@@ -219,8 +230,8 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lds0 = smem;
   float* lds1 = smem + G::LDS_LEN;
-  float* htab = smem + 2 * G::LDS_LEN;   // R tap rows
-  float* tail0 = htab + R * G::SPAN4;    // inputs of the block's last output (tile 0)
+  float* htab = smem + 2 * G::LDS_LEN;                 // R tap rows (TM 0)
+  float* tail0 = htab + (TM == 0 ? R * G::SPAN4 : 0);  // inputs of the block's last output (tile 0)
   float* tail1 = tail0 + G::TAIL;
 
   const int tid = threadIdx.x;
@@ -235,30 +246,23 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
   // tap rows, once per workgroup: htab[r][w] = h[HALO + D*r - w] (0 where
   // that k is not a tap)
-  for (int i = tid; i < R * G::SPAN4; i += NTH) {
-    const int r = i / G::SPAN4, w = i - r * G::SPAN4;
-    const int k = G::HALO + D * r - w;
-    htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
+  if constexpr (TM == 0) {
+    for (int i = tid; i < R * G::SPAN4; i += NTH) {
+      const int r = i / G::SPAN4, w = i - r * G::SPAN4;
+      const int k = G::HALO + D * r - w;
+      htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
+    }
   }
 
-  float4 v0[MODE == 0 ? G::FULL + 1 : 1], v1[MODE == 0 ? G::FULL + 1 : 1];
-  float hreg[MODE == 1 ? T : 1];
-  if constexpr (MODE == 0) {
+  using Stage = float4[G::FULL + 1];
+  Stage sa0, sa1;
 #pragma unroll
-    for (int i = 0; i <= G::FULL; ++i) v0[i] = v1[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // keeps them in VGPRs
-    if (a.ablate != 1)
-      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, v0, v1);
-  } else {
-    // taps into VGPRs once (uniform values): row 0 of the tap table holds
-    // h[HALO - w] at w
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < T; ++k) hreg[k] = htab[G::HALO - k];
-  }
+  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.ablate != 1)
+    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
 
-  for (int lin = first; lin < last; ++lin) {
+  auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
-
     // Old prev_I/prev_Q and the T inputs of the block's last decimated
     // sample (the prev_* carry source), read before this workgroup rewrites
     // state/prev at the end of the iteration.  D*(nout-1) - k >= -(T-1) >=
@@ -282,34 +286,14 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // ---- 1. registers -> LDS (after every read of the previous tile), then
     // prefetch the next tile into the registers just freed
     __syncthreads();
-    if constexpr (MODE == 0) {
-      stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
-    } else if (a.ablate != 1) {
-      // LDS-DMA: each wave-instruction moves 64 x 16 B = 1 KiB of the span
-      // straight into LDS (linear destination, per-lane source address)
-      typedef __attribute__((address_space(3))) void lds_t;
-      typedef __attribute__((address_space(1))) const void glb_t;
-#pragma unroll
-      for (int it = 0; it <= G::FULL; ++it) {
-        const int i = tid + it * NTH;
-        if (it < G::FULL || tid < G::REM) {
-          long long p = tr.pb + 4LL * i;
-          p = p < 0 ? 0 : (p > n - 4 ? n - 4 : p);
-          __builtin_amdgcn_global_load_lds((glb_t*)(tr.x0 + p), (lds_t*)(lds0 + 4 * (it * NTH)), 16, 0, 0);
-          __builtin_amdgcn_global_load_lds((glb_t*)(tr.x1 + p), (lds_t*)(lds1 + 4 * (it * NTH)), 16, 0, 0);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
     if (!interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
       fix_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
     }
     __syncthreads();
-    if constexpr (MODE == 0) {
-      if (lin + 1 < last && a.ablate != 1)
-        stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + 1), n, tid, v0, v1);
-    }
+    if (lin + PF < last && a.ablate != 1)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF), n, tid, v0, v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
@@ -335,58 +319,103 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
-      const float* ht = htab + (R - GR) * G::SPAN4;  // the top GR rows
-      float4 top[G::NCHUNK][GR];                     // compile-time indexed: SSA values
-      float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
-      float4 q1 = q0;
-      if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
-      if constexpr (MODE == 0) {
+      if constexpr (TM == 0) {
+        const float* ht = htab + (R - GR) * G::SPAN4;  // the top GR rows
+        float4 top[G::NCHUNK][GR];                     // compile-time indexed: SSA values
+        float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
+        float4 q1 = q0;
+        if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
 #pragma unroll
         for (int g = 0; g < GR; ++g) top[C0][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * C0);
-      }
 #pragma unroll
-      for (int c = C0; c >= 0; --c) {
-        float4 n0 = q0, n1 = q1;
-        if (c > 0) {
-          n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
-          if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
-          if constexpr (MODE == 0) {
+        for (int c = C0; c >= 0; --c) {
+          float4 n0 = q0, n1 = q1;
+          if (c > 0) {
+            n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
+            if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
 #pragma unroll
             for (int g = 0; g < GR; ++g)
               top[c - 1][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * (c - 1));
           }
-        }
-        const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
-        const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+          const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+          const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-        for (int j = 3; j >= 0; --j) {
-          const int w = 4 * c + j;  // window position; output r sits at HALO + D*r
+          for (int j = 3; j >= 0; --j) {
+            const int w = 4 * c + j;  // window position; output r sits at HALO + D*r
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int k = G::HALO + D * r - w;
-            if (k >= 0 && k < T) {
-              float hk;
-              if constexpr (MODE == 1) {
-                hk = hreg[k];
-              } else {
+            for (int r = 0; r < R; ++r) {
+              const int k = G::HALO + D * r - w;
+              if (k >= 0 && k < T) {
                 // row r at chunk c == top row r + m*GR at chunk c + m*SH
                 const int m = r >= R - GR ? 0 : (R - GR - r + GR - 1) / GR;
                 const float4 hv = top[c + m * SH][r + m * GR - (R - GR)];
-                hk = j == 0 ? hv.x : j == 1 ? hv.y : j == 2 ? hv.z : hv.w;
+                const float hk = j == 0 ? hv.x : j == 1 ? hv.y : j == 2 ? hv.z : hv.w;
+                acc0[r] = acc0[r] + hk * e0[j];
+                if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
               }
-              acc0[r] = acc0[r] + hk * e0[j];
-              if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
             }
           }
-        }
-        q0 = n0;
-        q1 = n1;
-        // Pin both channels' chains to this chunk: without it LLVM defers
-        // one channel's products past later chunks (holding their operands
-        // live -> 256 VGPRs at R = 4).
+          q0 = n0;
+          q1 = n1;
+          // Pin both channels' chains to this chunk: without it LLVM defers
+          // one channel's products past later chunks (holding their operands
+          // live -> 256 VGPRs at R = 4).
 #pragma unroll
-        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
-        __builtin_amdgcn_sched_barrier(0);
+          for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        // Taps as SGPR operands of the multiplies: no LDS tap traffic.  All
+        // T taps do not fit the SGPR file beside the addressing, so the
+        // window is walked in NPASS passes over consecutive tap ranges
+        // [k0, k1), each loading its taps once (scalar loads from the
+        // constant address space, one wait) -- every output still visits
+        // k = 0..T-1 in order, the passes only split its chain.
+        constexpr int NPASS = 3, KP = (T + NPASS - 1) / NPASS;
+        using hconst = const __attribute__((address_space(4))) float*;
+        const hconst hc = (hconst)h;
+        float hs[KP];
+        static_for<0, NPASS>([&](auto pi) {
+          constexpr int k0 = decltype(pi)::value * KP;
+          constexpr int k1 = k0 + KP < T ? k0 + KP : T;
+#pragma unroll
+          for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
+#pragma unroll
+          for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
+          // window positions w = HALO + D r - k this pass touches
+          constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
+          constexpr int whi = G::HALO + D * (R - 1) - k0;
+          constexpr int clo = wlo / 4, chi = whi / 4;
+          float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * chi);
+          float4 q1 = q0;
+          if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * chi);
+          static_for<0, chi - clo + 1>([&](auto ci) {
+            constexpr int c = chi - decltype(ci)::value;
+            float4 n0 = q0, n1 = q1;
+            if constexpr (c > clo) {
+              n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
+              if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+            }
+            const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+            const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+            static_for<0, 4>([&](auto ji) {
+              constexpr int j = 3 - decltype(ji)::value;
+              static_for<0, R>([&](auto ri) {
+                constexpr int r = decltype(ri)::value;
+                constexpr int k = G::HALO + D * r - (4 * c + j);
+                if constexpr (k >= k0 && k < k1) {
+                  acc0[r] = acc0[r] + hs[k - k0] * e0[j];
+                  if (NCH == 2) acc1[r] = acc1[r] + hs[k - k0] * e1[j];
+                }
+              });
+            });
+            q0 = n0;
+            q1 = n1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
+            __builtin_amdgcn_sched_barrier(0);
+          });
+        });
       }
     }
 
@@ -471,7 +500,9 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
         if (NCH == 2) tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
       }
     }
-  }
+  };
+
+  for (int lin = first; lin < last; ++lin) tile(lin, sa0, sa1);
 }
 
 // ---------------------------------------------------------- generic path --
@@ -547,7 +578,7 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 // ------------------------------------------------------------ dispatch ----
 // Persistent grid: about `waves_per_cu` single-wave workgroups per CU (or the
 // tile count, if smaller), each walking a contiguous run of tiles.
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int MODE = 0>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM = 0>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
@@ -564,7 +595,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
   static const int per_cu = [] {
     const char* e = std::getenv("SDR_WG_PER_CU");
     const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 48;
+    return v > 0 ? v : 32;
   }();
   const long long slots = (long long)ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
   const long long grid = total < slots ? total : slots;
@@ -575,17 +606,17 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
     return e ? std::atoi(e) : 0;
   }();
   a.ablate = ablate;
-  const size_t lds = (size_t)G::SMEM * sizeof(float);
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, MODE>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
+  const size_t lds = (size_t)(G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float);  // TM 1: no tap rows
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();
 }
 
 // Fast-path table: (R outputs per lane, NW waves per workgroup) per decimation
 // factor.  D*R must be a multiple of 4 (aligned lane windows).  The default
 // per D is the measured best on MI355X; SDR_FIR_VARIANT=<R>x<NW>
-// (e.g. "2x1") overrides it for experiments.
+// (e.g. "2x1": LDS tap rows) or <R>x<NW>r (SGPR taps) overrides it.
 struct Variant {
-  int R, NW, mode;  // mode: 0 register prefetch + LDS tap rows, 1 LDS-DMA + VGPR taps (f32 only)
+  int R, NW, tm;  // tm: taps in LDS rows (0) or DPP-broadcast VGPRs (1)
 };
 
 Variant variant_for(int D, bool demod) {
@@ -595,7 +626,7 @@ Variant variant_for(int D, bool demod) {
     char m = 0;
     const int got = std::sscanf(env, "%dx%d%c", &r, &w, &m);
     if (got >= 2) {
-      const Variant v{r, w, m == 'd' ? 1 : 0};
+      const Variant v{r, w, m == 'r' ? 1 : 0};
       const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
                          (D == 5 && r == 4 && (w == 1 || w == 4)) ||
                          (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
@@ -603,8 +634,8 @@ Variant variant_for(int D, bool demod) {
     }
   }
   switch (D) {
-    case 10: return {2, 1, 0};
-    case 5: return {4, 1, 0};
+    case 10: return {2, 1, 1};
+    case 5: return {4, 1, 1};
     case 1: return {4, 1, 0};
     default: return {0, 0, 0};
   }
@@ -626,13 +657,12 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
   const Variant v = variant_for(a.D, DEMOD);
   const int key = a.D * 10000 + v.R * 100 + v.NW;
   if (a.ntaps == 101) {
-    if constexpr (SRC == Src::F32) {
-      if (v.mode == 1) {
-        switch (key) {
-          case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st);
-          case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st);
-          default: break;
-        }
+    if (v.tm == 1) {
+      switch (key) {
+        case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st);
+        case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st);
+        case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st);
+        default: break;
       }
     }
     switch (key) {
