@@ -219,9 +219,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // TM = where the taps live: 0 LDS broadcast rows, 1 SGPRs (NPASS passes).
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM>
+// PF = prefetch depth: tile i+PF's loads are issued (into one of PF
+// register sets) before tile i is computed.
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, int PF>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
-  constexpr int PF = 1;
+  static_assert(PF == 1 || PF == 2, "prefetch depth");
   using G = Geom<D, T, R, DEMOD, NW>;
   constexpr int NTH = G::NTH;
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
@@ -240,8 +242,25 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   const long long nout = n / D;
   const int ns = a.ns;
   const int total = a.nstreams * a.tiles_per_stream;
-  const int first = blockIdx.x * a.tiles_per_wg;
-  const int last = min(first + a.tiles_per_wg, total);
+  // The tiles this workgroup walks: first, first + step, ... < last.
+  //  walk 0: a contiguous run of tiles_per_wg tiles;
+  //  walk 1: workgroups are dispatched to the 8 XCDs round-robin, so
+  //    XCD x = blockIdx % 8 owns the x-th eighth of all tiles and its
+  //    workgroups interleave through it: at any moment the resident
+  //    workgroups of one XCD stream adjacent tiles (DRAM page locality, and
+  //    each halo is the neighbour's tail, in the same L2).
+  int first, step, last;
+  if (a.walk == 0) {
+    first = blockIdx.x * a.tiles_per_wg;
+    step = 1;
+    last = min(first + a.tiles_per_wg, total);
+  } else {
+    const int per_xcd = (total + 7) / 8;
+    const int x = blockIdx.x & 7;
+    step = gridDim.x >> 3;
+    first = x * per_xcd + (blockIdx.x >> 3);
+    last = min((x + 1) * per_xcd, total);
+  }
   if (first >= last) return;
 
   // tap rows, once per workgroup: htab[r][w] = h[HALO + D*r - w] (0 where
@@ -255,11 +274,15 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   }
 
   using Stage = float4[G::FULL + 1];
-  Stage sa0, sa1;
+  Stage sa0, sa1, sb0, sb1;
 #pragma unroll
-  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.ablate != 1)
+  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = sb0[i] = sb1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.ablate != 1) {
     stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
+    if (PF == 2 && first + step < last)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first + step), n, tid, sb0,
+                                               sb1);
+  }
 
   auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
@@ -292,8 +315,9 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       fix_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
     }
     __syncthreads();
-    if (lin + PF < last && a.ablate != 1)
-      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF), n, tid, v0, v1);
+    if (lin + PF * step < last && a.ablate != 1)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF * step), n, tid, v0,
+                                               v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
@@ -502,7 +526,12 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     }
   };
 
-  for (int lin = first; lin < last; ++lin) tile(lin, sa0, sa1);
+  for (int lin = first; lin < last; lin += PF * step) {
+    tile(lin, sa0, sa1);
+    if constexpr (PF == 2) {
+      if (lin + step < last) tile(lin + step, sb0, sb1);
+    }
+  }
 }
 
 // ---------------------------------------------------------- generic path --
@@ -576,10 +605,10 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 }
 
 // ------------------------------------------------------------ dispatch ----
-// Persistent grid: about `waves_per_cu` single-wave workgroups per CU (or the
-// tile count, if smaller), each walking a contiguous run of tiles.
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM = 0>
-hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
+// Persistent grid: about `wpc` waves per CU (or the tile count, if smaller),
+// each workgroup walking its share of the tiles (see `walk` in fir_tile).
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM = 0, int PF = 1>
+hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
   const long long nout = a.n / D;
@@ -592,41 +621,58 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st) {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  static const int per_cu = [] {
+  static const int per_cu_env = [] {
     const char* e = std::getenv("SDR_WG_PER_CU");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 32;
+    return e ? std::atoi(e) : 0;
+  }();
+  const int per_cu = per_cu_env > 0 ? per_cu_env : wpc;
+  static const int walk = [] {
+    const char* e = std::getenv("SDR_TILE_WALK");
+    return e ? std::atoi(e) : 1;
   }();
   const long long slots = (long long)ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
-  const long long grid = total < slots ? total : slots;
-  a.tiles_per_wg = (int)((total + grid - 1) / grid);
-  const long long blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
+  long long blocks;
+  if (walk == 1 && total >= 8 * 8) {
+    // a multiple of 8 workgroups, none of them idle
+    a.walk = 1;
+    const long long per_xcd = (total + 7) / 8;
+    const long long g = (slots < per_xcd * 8 ? slots : per_xcd * 8) / 8;
+    blocks = 8 * (g > 0 ? g : 1);
+    a.tiles_per_wg = (int)((per_xcd + blocks / 8 - 1) / (blocks / 8));
+  } else {
+    a.walk = 0;
+    const long long grid = total < slots ? total : slots;
+    a.tiles_per_wg = (int)((total + grid - 1) / grid);
+    blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
+  }
   static const int ablate = [] {
     const char* e = std::getenv("SDR_ABLATE");
     return e ? std::atoi(e) : 0;
   }();
   a.ablate = ablate;
   const size_t lds = (size_t)(G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float);  // TM 1: no tap rows
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, PF>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();
 }
 
-// Fast-path table: (R outputs per lane, NW waves per workgroup) per decimation
-// factor.  D*R must be a multiple of 4 (aligned lane windows).  The default
-// per D is the measured best on MI355X; SDR_FIR_VARIANT=<R>x<NW>
-// (e.g. "2x1": LDS tap rows) or <R>x<NW>r (SGPR taps) overrides it.
+// Fast-path table: (R outputs per lane, NW waves per workgroup, tap mode,
+// prefetch depth, waves per CU) per decimation factor and input format.
+// D*R must be a multiple of 4 (aligned lane windows).  The defaults are the
+// measured best on MI355X; SDR_FIR_VARIANT=<R>x<NW>[r|p] (no
+// suffix: LDS tap rows; r: SGPR taps; p: SGPR taps + 2-deep prefetch) and
+// SDR_WG_PER_CU override them for experiments.
 struct Variant {
-  int R, NW, tm;  // tm: taps in LDS rows (0) or DPP-broadcast VGPRs (1)
+  int R, NW, tm, pf, wpc;  // tm: taps in LDS rows (0) or SGPRs (1); pf: prefetch depth
 };
 
-Variant variant_for(int D, bool demod) {
+Variant variant_for(int D, bool demod, Src src) {
   static const char* env = std::getenv("SDR_FIR_VARIANT");
   if (env) {
     int r = 0, w = 0;
     char m = 0;
     const int got = std::sscanf(env, "%dx%d%c", &r, &w, &m);
     if (got >= 2) {
-      const Variant v{r, w, m == 'r' ? 1 : 0};
+      const Variant v{r, w, m == 'r' || m == 'p' ? 1 : 0, m == 'p' ? 2 : 1, m == 'p' ? 24 : 32};
       const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
                          (D == 5 && r == 4 && (w == 1 || w == 4)) ||
                          (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
@@ -634,10 +680,10 @@ Variant variant_for(int D, bool demod) {
     }
   }
   switch (D) {
-    case 10: return {2, 1, 1};
-    case 5: return {4, 1, 1};
-    case 1: return {4, 1, 0};
-    default: return {0, 0, 0};
+    case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 2, 24} : Variant{2, 1, 1, 1, 32};
+    case 5: return {4, 1, 1, 1, 32};
+    case 1: return {4, 1, 0, 1, 32};
+    default: return {0, 0, 0, 1, 32};
   }
 }
 
@@ -654,31 +700,37 @@ bool geometry_ok(int D, int T, int ns, bool demod, Variant v) {
 template <int NCH, bool DEMOD, Src SRC>
 hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, bool* handled) {
   *handled = true;
-  const Variant v = variant_for(a.D, DEMOD);
+  const Variant v = variant_for(a.D, DEMOD, SRC);
   const int key = a.D * 10000 + v.R * 100 + v.NW;
   if (a.ntaps == 101) {
+    if (v.pf == 2) {
+      switch (key) {
+        case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 2>(a, h, st, v.wpc);
+        default: break;
+      }
+    }
     if (v.tm == 1) {
       switch (key) {
-        case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st);
-        case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st);
-        case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st);
+        case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         default: break;
       }
     }
     switch (key) {
-      case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC>(a, h, st);
-      case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC>(a, h, st);
-      case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st);
-      case 100402: return run_tile<10, 101, 4, 2, NCH, DEMOD, SRC>(a, h, st);
-      case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st);
-      case 50404: return run_tile<5, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st);
+      case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+      case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+      case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+      case 100402: return run_tile<10, 101, 4, 2, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+      case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+      case 50404: return run_tile<5, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st, v.wpc);
       default: break;
     }
     if constexpr (!DEMOD && NCH == 1) {
       switch (key) {
-        case 10401: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st);
-        case 10404: return run_tile<1, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st);
-        case 10801: return run_tile<1, 101, 8, 1, NCH, DEMOD, SRC>(a, h, st);
+        case 10401: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+        case 10404: return run_tile<1, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+        case 10801: return run_tile<1, 101, 8, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
         default: break;
       }
     }
@@ -694,7 +746,7 @@ bool fir_has_fast_path(int D, int ntaps, int ns, int nch, bool demod, Src src) {
   if (src == Src::U8 && (nch != 2 || !demod)) return false;
   if (demod != (nch == 2)) return false;  // instantiated: fused 2-channel, or 1-channel FIR
   if (D != 10 && D != 5 && !(D == 1 && !demod)) return false;
-  return geometry_ok(D, ntaps, ns, demod, variant_for(D, demod));
+  return geometry_ok(D, ntaps, ns, demod, variant_for(D, demod, src));
 }
 
 hipError_t launch_demod(const float* I, const float* Q, long long n, int nstreams, long long stride, float* prev_i,

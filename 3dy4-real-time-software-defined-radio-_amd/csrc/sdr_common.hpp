@@ -41,7 +41,8 @@ struct FirLaunch {
   float* out;
   long long out_stride;
   int tiles_per_stream;
-  int tiles_per_wg;  // persistent tile kernels: contiguous tiles per workgroup
+  int tiles_per_wg;  // persistent tile kernels: tiles per workgroup
+  int walk;          // 0: each workgroup walks contiguous tiles; 1: XCD-strided (see fir_tile.hip)
   int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math
 };
 
