@@ -59,9 +59,11 @@ struct Geom {
   static constexpr int LDS_LEN = D * ((NW - 1) * WADV + 63 * R) + SPAN4;  // floats per channel
   static constexpr int LDS4 = LDS_LEN / 4;
   static constexpr int FULL = LDS4 / NTH, REM = LDS4 % NTH;        // staging rows per thread
-  static constexpr int TAIL = (T + 3) / 4 * 4;                     // prev_* recompute strip
+  // the block's last STRIP inputs per channel, staged by tile 0: the
+  // prev_* recompute (D+T-1 inputs) and the new state (ns <= STRIP)
+  static constexpr int STRIP = ((D + T - 1 > 128 ? D + T - 1 : 128) + 3) / 4 * 4;
   // LDS floats: channels, tap rows, two tail strips
-  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4 + 2 * TAIL;
+  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4 + 2 * STRIP;
 };
 
 __device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp) {
@@ -134,15 +136,19 @@ __device__ __forceinline__ TileRef tile_ref(const FirLaunch& a, int lin) {
   return r;
 }
 
-// A tile whose whole span lies inside the block: no state, no tail.
+// A tile no clamped chunk of which holds a sample a stored output reads:
+// its span starts at p >= 0 and, when n is not a multiple of 4, ends before
+// the chunk straddling n.  (Chunks past n only feed outputs >= n/D, which
+// are never stored.)
 template <int D, int T, int R, bool DEMOD, int NW>
 __device__ __forceinline__ bool interior(const TileRef& tr, long long n) {
-  return tr.pb >= 0 && tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n;
+  const long long n4 = n & ~3LL;
+  return tr.pb >= 0 && (n4 == n || tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n4);
 }
 
 // Issue every global load of one tile span into registers (16-B f32 / 8-B
 // u8 coalesced vectors).  Chunk addresses are clamped into the block, so an
-// edge tile loads in-bounds but partly wrong data that fix_edge() then
+// edge tile loads in-bounds but partly wrong data that edge_fill() then
 // overwrites.  No wait: stage_store consumes the registers.
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
 __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int tid,
@@ -150,8 +156,9 @@ __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int t
                                            float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   using G = Geom<D, T, R, DEMOD, NW>;
   auto load4 = [&](int i, float4& a0, float4& a1) {
+    const long long pmax = (n & ~3LL) - 4;  // last whole aligned chunk
     long long p = tr.pb + 4LL * i;
-    p = p < 0 ? 0 : (p > n - 4 ? n - 4 : p);
+    p = p < 0 ? 0 : (p > pmax ? pmax : p);
     if constexpr (SRC == Src::F32) {
       a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
       if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
@@ -170,22 +177,61 @@ __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int t
   if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
 }
 
-// First / last tile of a stream (about 2 in every tiles_per_stream): after
-// the clamped vector fill, rewrite the span elements whose chunk was clamped
-// -- the old state before the block, the true samples of the chunk
-// straddling its end (n need not be a multiple of 4), zeros past it (they
-// never reach a stored output).  The tile span starts 16-B aligned, so no
-// chunk straddles position 0.
+// Edge tiles (a stream's first tile, and the one holding the chunk that
+// straddles n when n % 4 != 0): after the clamped vector fill, rewrite the
+// span elements a stored output reads whose chunk was clamped -- the old
+// state before the block, [pb, 0), and the true samples of the straddling
+// chunk, [n & ~3, n).  With `strip`, also stage the block's last STRIP
+// inputs (old state where p < 0) for tile 0's state carry.  The loads are
+// issued in batches of four per thread before any LDS write, so an edge tile
+// costs about one memory latency, not one per element.
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
-__device__ __forceinline__ void fix_edge(const TileRef& tr, int tid, long long n, int ns, float* lds0,
-                                         float* lds1) {
+__device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long n, int ns, float* lds0, float* lds1,
+                                          bool strip, float* strip0, float* strip1) {
   using G = Geom<D, T, R, DEMOD, NW>;
-  const long long tail_from = (n - 4) & ~3LL;  // no clamped chunk starts below min(n-4 rounded, ...)
-  for (int i = tid; i < G::LDS_LEN; i += G::NTH) {
-    const long long p = tr.pb + i;
-    if (p < 0 || p >= tail_from) {
-      lds0[i] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
-      if (NCH == 2) lds1[i] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+  const long long n4 = n & ~3LL;
+  const int lo_end = tr.pb < 0 ? (int)(-tr.pb < G::LDS_LEN ? -tr.pb : G::LDS_LEN) : 0;
+  auto clampi = [](long long v, int lo, int hi) { return (int)(v < lo ? lo : (v > hi ? hi : v)); };
+  const int hi_beg = clampi(n4 - tr.pb, lo_end, G::LDS_LEN);
+  const int hi_end = clampi(n - tr.pb, hi_beg, G::LDS_LEN);
+  const int nfix = lo_end + (hi_end - hi_beg);
+  const int ntot = nfix + (strip ? G::STRIP : 0);
+  for (int e0 = 0; e0 < ntot; e0 += 4 * G::NTH) {
+    float v0[4], v1[4];
+    float* d0[4];
+    float* d1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * G::NTH + tid;
+      long long p;
+      if (e < lo_end) {
+        p = tr.pb + e;
+        d0[u] = lds0 + e;
+        d1[u] = lds1 + e;
+      } else if (e < nfix) {
+        const int i = hi_beg + (e - lo_end);
+        p = tr.pb + i;
+        d0[u] = lds0 + i;
+        d1[u] = lds1 + i;
+      } else {
+        const int j = e - nfix;
+        p = n - G::STRIP + j;
+        d0[u] = strip0 + j;
+        d1[u] = strip1 + j;
+      }
+      v0[u] = 0.0f;
+      v1[u] = 0.0f;
+      if (e < ntot) {
+        v0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+        if (NCH == 2) v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * G::NTH + tid < ntot) {
+        *d0[u] = v0[u];
+        if (NCH == 2) *d1[u] = v1[u];
+      }
     }
   }
 }
@@ -233,8 +279,8 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   float* lds0 = smem;
   float* lds1 = smem + G::LDS_LEN;
   float* htab = smem + 2 * G::LDS_LEN;                 // R tap rows (TM 0)
-  float* tail0 = htab + (TM == 0 ? R * G::SPAN4 : 0);  // inputs of the block's last output (tile 0)
-  float* tail1 = tail0 + G::TAIL;
+  float* strip0 = htab + (TM == 0 ? R * G::SPAN4 : 0);  // the block's last inputs (tile 0)
+  float* strip1 = strip0 + G::STRIP;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -286,33 +332,26 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
   auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
-    // Old prev_I/prev_Q and the T inputs of the block's last decimated
-    // sample (the prev_* carry source), read before this workgroup rewrites
-    // state/prev at the end of the iteration.  D*(nout-1) - k >= -(T-1) >=
-    // -ns, so the old state covers p < 0.
+    // Old prev_I/prev_Q, read before this workgroup rewrites them at the
+    // end of the iteration (tile 0 only).
     float old_pi = 0.0f, old_pq = 0.0f;
     if constexpr (DEMOD) {
-      if (tr.t == 0) {
-        if (tid == 1) {
-          old_pi = a.prev0[tr.s];
-          old_pq = a.prev1[tr.s];
-        }
-        const long long P = (long long)D * (nout - 1);
-        for (int k = tid; k < T; k += NTH) {
-          const long long p = P - k;
-          tail0[k] = p < 0 ? tr.st0[ns + p] : in_at<SRC>(tr.x0, tr.iq, 0, p);
-          tail1[k] = p < 0 ? tr.st1[ns + p] : in_at<SRC>(tr.x1, tr.iq, 1, p);
-        }
+      if (tr.t == 0 && tid == 1) {
+        old_pi = a.prev0[tr.s];
+        old_pq = a.prev1[tr.s];
       }
     }
 
     // ---- 1. registers -> LDS (after every read of the previous tile), then
-    // prefetch the next tile into the registers just freed
+    // prefetch the next tile into the registers just freed.  Tile 0 also
+    // stages the block's last STRIP inputs (old state where p < 0: the
+    // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
+    // rewrites the state below.
     __syncthreads();
     stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
-    if (!interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
+    if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
-      fix_edge<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1);
+      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, tr.t == 0, strip0, strip1);
     }
     __syncthreads();
     if (lin + PF * step < last && a.ablate != 1)
@@ -505,23 +544,31 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     if (tr.t == 0) {
       if constexpr (DEMOD) {
         // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
-        // recomputed in the reference's order from the staged strip
+        // recomputed in the reference's order from the staged strip:
+        // input D*(nout-1) - k = n - D - k sits at strip index STRIP - D - k
         if (tid == 0) {
           float yi = 0.0f, yq = 0.0f;
           for (int k = 0; k < T; ++k) {
             const float hk = h[k];
-            yi = yi + hk * tail0[k];
-            yq = yq + hk * tail1[k];
+            yi = yi + hk * strip0[G::STRIP - D - k];
+            yq = yq + hk * strip1[G::STRIP - D - k];
           }
           a.prev0[tr.s] = yi;
           a.prev1[tr.s] = yq;
         }
       }
       // state <- last ns input samples (src/filter.cpp:139)
-      for (int j = tid; j < ns; j += NTH) {
-        const long long p = n - ns + j;
-        tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, p);
-        if (NCH == 2) tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
+      if (ns <= G::STRIP) {
+        for (int j = tid; j < ns; j += NTH) {
+          tr.st0[j] = strip0[G::STRIP - ns + j];
+          if (NCH == 2) tr.st1[j] = strip1[G::STRIP - ns + j];
+        }
+      } else {
+        for (int j = tid; j < ns; j += NTH) {
+          const long long p = n - ns + j;
+          tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, p);
+          if (NCH == 2) tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
+        }
       }
     }
   };

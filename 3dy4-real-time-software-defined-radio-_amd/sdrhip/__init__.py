@@ -25,7 +25,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libsdrhip.so")
+# SDRHIP_LIB: another build of the same C ABI (A/B timing of kernel
+# revisions, scripts/build_ab.sh); the in-tree library otherwise.
+LIB_PATH = os.environ.get("SDRHIP_LIB") or os.path.join(PKG_DIR, "libsdrhip.so")
 DROPIN_PATH = os.path.join(PKG_DIR, "libdy4filter_hip.so")
 REPO_DIR = os.path.dirname(PKG_DIR)
 HEADER_PATH = os.path.join(REPO_DIR, "include", "sdr_hip.h")

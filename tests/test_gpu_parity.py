@@ -112,6 +112,30 @@ def test_fir_decim_vs_oracle(gpu_ctx, oracle, D, ntaps, ns, n):
         assert_bits(s_g, s_o, "state")
 
 
+@pytest.mark.parametrize("D,n,ns", [(10, 5130, 100), (10, 5130, 150), (10, 2000, 200), (5, 4105, 100),
+                                    (5, 4105, 128), (10, 110, 100), (10, 200, 180)])
+def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, D, n, ns):
+    """Fused front end (f32 and u8 wire) where the tiled kernel's edge
+    handling matters: n % 4 != 0 (a chunk straddles the block end), state
+    lengths below and above the kernel's staged strip, blocks barely longer
+    than the state (the last output's inputs reach into the old state)."""
+    from sdrhip.synth import fm_iq_u8
+
+    h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
+    iq = fm_iq_u8(n * 3, seed=D * 100 + n + ns)
+    st = {k: [np.zeros(ns, np.float32), np.zeros(ns, np.float32), np.zeros(2, np.float32)]
+          for k in ("f32", "u8", "oracle")}
+    for b in range(3):
+        blk = iq[2 * n * b:2 * n * (b + 1)]
+        I, Q = oracle.u8_to_planar(blk)
+        want = oracle.frontend(D, I, Q, h, *st["oracle"])
+        assert_bits(gpu_ctx.frontend(D, I, Q, h, *st["f32"]), want, f"f32 block {b}")
+        assert_bits(gpu_ctx.frontend_u8(D, blk, h, *st["u8"]), want, f"u8 block {b}")
+        for k in ("f32", "u8"):
+            for got, ref, what in zip(st[k], st["oracle"], ("state_i", "state_q", "prev")):
+                assert_bits(got, ref, f"{k} {what} block {b}")
+
+
 @pytest.mark.parametrize("up,down,ntaps,ns,n", [(147, 800, 22197, 150, 1600), (2, 3, 61, 30, 999),
                                                  (3, 8, 301, 150, 1600), (5, 2, 100, 20, 400)])
 def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
