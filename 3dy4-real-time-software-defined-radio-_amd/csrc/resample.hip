@@ -17,6 +17,9 @@
 // polyphase table hp[p][i] = h[p + i*up] (built once per call into device
 // scratch) so each lane streams its branch contiguously (16-B loads, L1/L2
 // resident: the whole table is T floats).
+#include <cstdlib>
+#include <type_traits>
+
 #include "sdr_common.hpp"
 
 #pragma clang fp contract(off)
@@ -75,6 +78,206 @@ __global__ __launch_bounds__(kWG) void resample_tile(const float* __restrict__ x
   y[(long long)s * y_stride + j] = acc;
 }
 
+// ------------------------------------------------ phase-major tiled kernel --
+// For T == CMAX*up (every phase has exactly CMAX taps: the reference's
+// num_taps*up convention, src/project.cpp:210) and up >= 2.
+//
+// Output j = up*t + phi has phase p = (phi*down) mod up and newest input
+// q = t*down + (phi*down) div up: the phase depends on phi only.  A
+// "column" is one period t of one stream (up consecutive outputs); a
+// workgroup takes 64 columns (one per lane) x NW consecutive phi (one per
+// wave).  Within a wave the taps are therefore uniform -- SGPR operands,
+// loaded per pass of KP taps like fir_tile -- and each lane slides down its
+// own window with 16-B LDS reads.  Each lane's window lives in its own LDS
+// segment: inputs [t*down + q(phi0) - (CMAX-1) - sa, t*down + q(phi_last)],
+// the union of its NW outputs' windows, 16-B aligned (sa) when down % 4 == 0;
+// segment stride SEGPAD floats with SEGPAD/4 odd, so the 16-lane groups of
+// ds_read_b128 never share a bank.
+constexpr int kPPLanes = 64;
+
+template <int CMAX, int A, int I0, int I1>
+__device__ __forceinline__ void pp_pass(float& acc, const float* wl, int ctop, const float* hs) {
+  // element of tap i: LDS index 4*(ctop - cc) + jj with i = 4*cc + A - jj
+  constexpr int CLO = (I0 - A) > 0 ? (I0 - A + 3) / 4 : 0;
+  constexpr int CHI = (I1 + 2 - A) / 4;
+  float4 q = *reinterpret_cast<const float4*>(wl + 4 * (ctop - CLO));
+#pragma unroll
+  for (int cc = CLO; cc <= CHI; ++cc) {
+    float4 nx = q;
+    if (cc < CHI) nx = *reinterpret_cast<const float4*>(wl + 4 * (ctop - cc - 1));
+    const float e[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int jj = 3; jj >= 0; --jj) {
+      const int i = 4 * cc + A - jj;
+      if (i >= I0 && i < I1) acc = acc + hs[i - I0] * e[jj];
+    }
+    q = nx;
+    asm volatile("" : "+v"(acc));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int CMAX, int A>
+__device__ __forceinline__ float pp_scan(const float* wl, int ctop, const float* __restrict__ hrow) {
+  constexpr int KP = 32;
+  using hconst = const __attribute__((address_space(4))) float*;
+  const hconst hc = (hconst)hrow;
+  float acc = 0.0f;
+  float hs[KP];
+  auto pass = [&](auto i0c) {
+    constexpr int I0 = decltype(i0c)::value;
+    constexpr int I1 = I0 + KP < CMAX ? I0 + KP : CMAX;
+#pragma unroll
+    for (int i = 0; i < I1 - I0; ++i) hs[i] = hc[I0 + i];
+#pragma unroll
+    for (int i = 0; i < I1 - I0; ++i) asm volatile("" : "+s"(hs[i]));
+    pp_pass<CMAX, A, I0, I1>(acc, wl, ctop, hs);
+  };
+  pass(std::integral_constant<int, 0>{});
+  if constexpr (CMAX > KP) pass(std::integral_constant<int, KP>{});
+  if constexpr (CMAX > 2 * KP) pass(std::integral_constant<int, 2 * KP>{});
+  if constexpr (CMAX > 3 * KP) pass(std::integral_constant<int, 3 * KP>{});
+  if constexpr (CMAX > 4 * KP) pass(std::integral_constant<int, 4 * KP>{});
+  if constexpr (CMAX > 5 * KP) pass(std::integral_constant<int, 5 * KP>{});
+  static_assert(CMAX <= 6 * KP, "more tap passes");
+  return acc;
+}
+
+struct PPArgs {
+  const float* x;
+  long long n, x_stride;
+  const float* hp;  // polyphase table, row stride cpad
+  int cpad, up, down;
+  const float* state;
+  int ns;
+  float* y;
+  long long y_stride, ny;
+  int np;          // periods per stream
+  long long ncols; // nstreams * np
+  int nphg;        // phase groups (ceil(up / NW))
+  int segpad;      // LDS floats per lane segment
+  int vec;         // 16-B staging (down % 4 == 0 and aligned rows)
+  int ablate;      // timing experiments only (SDR_ABLATE): 1 = no staging, 2 = no taps walk
+};
+
+constexpr int kPPSeg = 260;  // max LDS floats per column segment (host-checked)
+
+// LDS image of one tile: kPPLanes column segments of a.segpad floats.
+// Interior 16-B chunks arrive by LDS-DMA (lane k of a wave-instruction
+// lands at segment base + 16*k, one instruction per column); the chunks
+// that reach before the block (state) or past its end go through registers
+// in pp_edge(), issued after the tile in flight has been computed.
+template <int CMAX>
+__device__ __forceinline__ void pp_dma(const PPArgs& a, long long cb, float* buf, int wv, int ln, int nw,
+                                       long long q0, int sa, int per_col) {
+  for (int cl = wv; cl < kPPLanes; cl += nw) {
+    const long long col = cb * kPPLanes + cl;
+    if (col >= a.ncols) break;
+    const long long sidx = col / a.np, t = col - sidx * a.np;
+    const long long g = t * a.down + q0 - (CMAX - 1) - sa + 4 * ln;  // multiple of 4
+    if (ln < per_col && g >= 0 && g + 4 <= a.n)
+      __builtin_amdgcn_global_load_lds(a.x + sidx * a.x_stride + g, buf + cl * a.segpad, 16, 0, 0);
+  }
+}
+
+template <int CMAX>
+__device__ __forceinline__ void pp_edge(const PPArgs& a, long long cb, float* buf, int wv, int ln, int nw,
+                                        long long q0, int sa, int per_col) {
+  for (int cl = wv; cl < kPPLanes; cl += nw) {
+    const long long col = cb * kPPLanes + cl;
+    if (col >= a.ncols) break;
+    const long long sidx = col / a.np, t = col - sidx * a.np;
+    const long long g = t * a.down + q0 - (CMAX - 1) - sa + 4 * ln;
+    if (ln < per_col && !(g >= 0 && g + 4 <= a.n)) {
+      const float* xs = a.x + sidx * a.x_stride;
+      const float* st = a.state + sidx * a.ns;
+      float w4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long gg = g + r;
+        w4[r] = gg >= 0 ? (gg < a.n ? xs[gg] : 0.0f) : (gg >= -a.ns ? st[a.ns + gg] : 0.0f);
+      }
+      *reinterpret_cast<float4*>(buf + cl * a.segpad + 4 * ln) = make_float4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  }
+}
+
+// Persistent: workgroup b keeps one phase group (its waves' phases, hence
+// their SGPR tap rows, stay fixed and scalar-cache hot) and walks a run of
+// column blocks with two LDS images: the DMA of block i+1 is in flight
+// while block i is computed.  The two images are distinct __shared__
+// objects, so the compiler's wait for the DMA does not hold the ds_reads of
+// the other image.
+template <int CMAX>
+__global__ __launch_bounds__(1024, 1) void resample_pp(PPArgs a) {
+  __shared__ __attribute__((aligned(16))) float imgA[kPPLanes * kPPSeg];
+  __shared__ __attribute__((aligned(16))) float imgB[kPPLanes * kPPSeg];
+  const int nw = blockDim.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+  const int grp = blockIdx.x % a.nphg;
+  const int slot = blockIdx.x / a.nphg, nslots = gridDim.x / a.nphg;
+  const long long ncb = (a.ncols + kPPLanes - 1) / kPPLanes;
+  const long long per = (ncb + nslots - 1) / nslots;
+  const long long cb0 = (long long)slot * per;
+  const long long cb1 = cb0 + per < ncb ? cb0 + per : ncb;
+  if (cb0 >= cb1) return;
+  const int phi0 = grp * nw;
+  const int phi_last = min(phi0 + nw, a.up) - 1;
+  const long long q0 = ((long long)phi0 * a.down) / a.up;
+  const long long qlast = ((long long)phi_last * a.down) / a.up;
+  const int sa = (int)(((q0 - (CMAX - 1)) % 4 + 4) % 4);  // 16-B align the segment start
+  const int seglen = (int)(qlast - q0) + CMAX + sa;
+  const int per_col = (seglen + 3) >> 2;
+  // this wave's phase (idle waves past the last phase still stage and sync)
+  const int phi = phi0 + wv;
+  const bool wave_on = phi <= phi_last;
+  const int p = (int)(((long long)phi * a.down) % a.up);
+  const int off = (int)(((long long)phi * a.down) / a.up - q0);
+  const int e1 = off + CMAX - 1 + sa;  // segment element of tap i = 0 (newest input)
+  const int A = e1 & 3, ctop = e1 >> 2;
+  const float* hrow = a.hp + (long long)(wave_on ? p : 0) * a.cpad;
+
+  auto compute = [&](long long cb, const float* img) __attribute__((always_inline)) {
+    if (!wave_on || a.ablate == 2) return;
+    const long long col = cb * kPPLanes + ln;
+    const long long sidx = col / a.np, t = col - sidx * a.np;
+    const long long j = (long long)a.up * t + phi;
+    const float* wl = img + ln * a.segpad;
+    float acc;
+    switch (A) {  // wave-uniform
+      case 0: acc = pp_scan<CMAX, 0>(wl, ctop, hrow); break;
+      case 1: acc = pp_scan<CMAX, 1>(wl, ctop, hrow); break;
+      case 2: acc = pp_scan<CMAX, 2>(wl, ctop, hrow); break;
+      default: acc = pp_scan<CMAX, 3>(wl, ctop, hrow); break;
+    }
+    if (col < a.ncols && j < a.ny) a.y[sidx * a.y_stride + j] = acc;
+  };
+  auto stage = [&](long long cb, float* img, bool edge) __attribute__((always_inline)) {
+    if (a.ablate == 1) return;
+    if (edge)
+      pp_edge<CMAX>(a, cb, img, wv, ln, nw, q0, sa, per_col);
+    else
+      pp_dma<CMAX>(a, cb, img, wv, ln, nw, q0, sa, per_col);
+  };
+
+  stage(cb0, imgA, false);
+  stage(cb0, imgA, true);
+  __syncthreads();
+  for (long long cb = cb0; cb < cb1; cb += 2) {
+    const bool nxt = cb + 1 < cb1;
+    if (nxt) stage(cb + 1, imgB, false);
+    compute(cb, imgA);
+    if (nxt) stage(cb + 1, imgB, true);
+    __syncthreads();  // image B landed; every wave is done reading A
+    if (!nxt) break;
+    const bool nxt2 = cb + 2 < cb1;
+    if (nxt2) stage(cb + 2, imgA, false);
+    compute(cb + 1, imgB);
+    if (nxt2) stage(cb + 2, imgA, true);
+    __syncthreads();
+  }
+}
+
 // Fallback when the staged window would not fit LDS (huge down/up ratios):
 // the same sum straight from global memory.
 __global__ __launch_bounds__(kWG) void resample_direct(const float* __restrict__ x, long long n, long long x_stride,
@@ -109,6 +312,14 @@ __global__ __launch_bounds__(kWG) void resample_commit(const float* __restrict__
   state[(long long)s * ns + i] = x[(long long)s * x_stride + n - ns + i];
 }
 
+bool pp_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SDR_RESAMPLE_PP");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 }  // namespace
 
 size_t resample_scratch_floats(int up, int ntaps) {
@@ -125,8 +336,65 @@ hipError_t launch_resample(int up, int down, const float* x, long long n, int ns
                      scratch_taps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const dim3 grid((unsigned)((ny + kWG - 1) / kWG), (unsigned)nstreams);
   const int cnt_max = (ntaps + up - 1) / up;
+  // phase-major tiled kernel: every phase has exactly cnt_max taps
+  if (up >= 2 && ntaps == cnt_max * up && (cnt_max == 151 || cnt_max == 101) && pp_enabled()) {
+    PPArgs a;
+    a.x = x;
+    a.n = n;
+    a.x_stride = x_stride;
+    a.hp = scratch_taps;
+    a.cpad = cmax;
+    a.up = up;
+    a.down = down;
+    a.state = state;
+    a.ns = ns;
+    a.y = y;
+    a.y_stride = y_stride;
+    a.ny = ny;
+    a.np = (int)((ny + up - 1) / up);
+    a.ncols = (long long)a.np * nstreams;
+    const int nw = up < 16 ? up : 16;
+    a.nphg = (up + nw - 1) / nw;
+    const long long qspan = ((long long)(nw - 1) * down + up - 1) / up + 1;  // >= q(phi_last) - q(phi0)
+    int segpad = (int)((qspan + cnt_max + 3 + 3) / 4 * 4);
+    if ((segpad / 4) % 2 == 0) segpad += 4;
+    a.segpad = segpad;
+    a.vec = (down % 4 == 0) && x_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    static const int ablate = [] {
+      const char* e = std::getenv("SDR_ABLATE");
+      return e ? std::atoi(e) : 0;
+    }();
+    a.ablate = ablate;
+    const long long seglen_max = qspan + cnt_max + 3;  // one DMA wave-instruction per column
+    if (segpad <= kPPSeg && seglen_max <= 256 && a.vec) {
+      static int ncu = 0;
+      if (!ncu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+          ncu = 256;
+      }
+      const long long ncb = (a.ncols + kPPLanes - 1) / kPPLanes;
+      long long slots = ncu / a.nphg;  // ~one workgroup per CU
+      if (slots < 1) slots = 1;
+      if (slots > ncb) slots = ncb;
+      const long long grid = slots * a.nphg;
+      if (cnt_max == 151)
+        hipLaunchKernelGGL(resample_pp<151>, dim3((unsigned)grid), dim3(64 * nw), 0, st, a);
+      else
+        hipLaunchKernelGGL(resample_pp<101>, dim3((unsigned)grid), dim3(64 * nw), 0, st, a);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      if (ns > 0) {
+        hipLaunchKernelGGL(resample_commit, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st, x, n,
+                           x_stride, state, ns);
+        e = hipGetLastError();
+      }
+      return e;
+    }
+  }
+  const dim3 grid((unsigned)((ny + kWG - 1) / kWG), (unsigned)nstreams);
   // widest staged window: 256 outputs span (255*down)/up + 1 inputs + taps
   const long long span = (255LL * down) / up + 2 + cmax;
   if (span <= kMaxSpan && cnt_max <= cmax) {

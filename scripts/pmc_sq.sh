@@ -20,4 +20,4 @@ ${GROUPS_OVERRIDE:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_IN
 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA
 GRBM_GUI_ACTIVE GRBM_COUNT}
 GROUPS
-python3 scripts/pmc_summary.py "$OUT" fir_tile | tee "$OUT/summary.txt"
+python3 scripts/pmc_summary.py "$OUT" ${KERNEL:-fir_tile} | tee "$OUT/summary.txt"

@@ -149,6 +149,34 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
         assert_bits(s_g, s_o, "state")
 
 
+@pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560),
+                                               (3, 7, 101, 100, 700), (5, 2, 151, 150, 400),
+                                               (147, 800, 151, 150, 65600)])
+def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, n):
+    """Phase-major tiled resampler (T = cnt*up): several streams per launch
+    (64-column blocks cross stream boundaries), 16-B and dword staging
+    (down % 4), up < 16 phase groups, multi-block state carry."""
+    sdrhip = built_lib
+    nstreams = 5 if n < 10000 else 2
+    rng = np.random.default_rng(up * 1000 + down)
+    h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
+    ny = sdrhip.resample_out_len(up, down, n)
+    states = [rng.standard_normal(ns).astype(np.float32) for _ in range(nstreams)]
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_st = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.stack(states))
+    y_stride = ny + 3
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * y_stride * 4)
+    for blk in range(2):
+        x = rng.standard_normal((nstreams, n)).astype(np.float32)
+        d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+        gpu_ctx.resample_dev(up, down, d_x, n, nstreams, n, d_h, len(h), d_st, ns, d_y, y_stride)
+        gpu_ctx.synchronize()
+        got = d_y.download().reshape(nstreams, y_stride)[:, :ny]
+        for s in range(nstreams):
+            assert_bits(got[s], oracle.resample(up, down, x[s], h, states[s]), f"stream {s} block {blk}")
+        assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
+
+
 # ------------------------------------------------------- batched device API
 
 def _fm_streams(nstreams, n, seed=5):
