@@ -820,6 +820,8 @@ hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, S
     }
     if (handled) return e;
   }
+  if (allow_fast && !demod && nch == 1 && src == Src::F32 && fir_long_ok(a.D, a.ntaps, a.ns, a.n))
+    return launch_fir_long(a, h, st);
   // generic: FIR (+ separate state commit) (+ separate demod)
   const long long nout = a.n / a.D;
   float* y0 = demod ? scratch_y0 : a.y0;

@@ -65,6 +65,10 @@ hipError_t launch_synth_fm_u8(uint8_t* iq, long long npairs, int nstreams, long 
 hipError_t launch_u8_to_planar(const uint8_t* iq, long long npairs, int nstreams, long long iq_stride, float* I,
                                float* Q, long long x_stride, hipStream_t st);
 
+// Long FIRs without decimation (fir_long.hip): T a multiple of 32.
+bool fir_long_ok(int D, int ntaps, int ns, long long n);
+hipError_t launch_fir_long(const FirLaunch& a, const float* h, hipStream_t st);
+
 // Whether the tiled fast path handles (D, ntaps, ns) for this source; false
 // means launch_fir takes the generic path (still exact, slower).
 bool fir_has_fast_path(int D, int ntaps, int ns, int nch, bool demod, Src src);
