@@ -393,6 +393,34 @@ int sdr_resample_f32_dev(sdr_ctx* c, int up, int down, const float* x, long long
   return SDR_OK;
 }
 
+int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,
+                          int ntaps, void* state, int ns, float* y, long long y_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
+  if (ntaps < 1 || nstreams < 1 || n <= 0) return fail(c, SDR_EINVAL, "empty taps/streams/block");
+  if (ns < ntaps - 1) return fail(c, SDR_EINVAL, "state length %d < ntaps-1 = %d (filter.cpp:74)", ns, ntaps - 1);
+  if (n < ns) return fail(c, SDR_EINVAL, "block length %lld < state length %d (filter.cpp:82)", n, ns);
+  if (nstreams > 1 && (x_stride < n || y_stride < n)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (nstreams > 1 && x_stride % 8))
+    return fail(c, SDR_EINVAL, "fp16 input rows must be 16-B aligned (x_stride %% 8 == 0)");
+  uint32_t* pairs = static_cast<uint32_t*>(scratch(c, kTmp, sdr::fir_long_h_pairs(ntaps) * sizeof(uint32_t)));
+  if (!pairs) return fail(c, SDR_ENOMEM, "tap pair table");
+  hipError_t e = sdr::launch_fir_long_h(x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, pairs, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "fir_block_f16 launch");
+  return SDR_OK;
+}
+
+int sdr_f32_to_f16_dev(sdr_ctx* c, const float* x, long long count, void* y) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!x || !y || count < 0) return fail(c, SDR_EINVAL, "bad conversion arguments");
+  if (count == 0) return SDR_OK;
+  hipError_t e = sdr::launch_f32_to_f16(x, count, y, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "f32_to_f16 launch");
+  return SDR_OK;
+}
+
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
                         unsigned long long seed) {
   int rc = enter(c);

@@ -166,4 +166,182 @@ hipError_t launch_fir_long(const FirLaunch& f, const float* h, hipStream_t st) {
   return hipGetLastError();
 }
 
+
+// ------------------------------------------------------------------ fp16 --
+// BASELINE config 5's fp16 arm: the same long FIR on fp16 storage (inputs,
+// state and taps rounded to fp16), fp32 accumulation with
+// v_dot2_f32_f16 -- two taps per instruction, a quarter of the exact
+// path's instruction count.  NOT bit-exact by construction (fp16 operands,
+// fused dot): its error against the fp32 reference is what the tolerance
+// sweep reports (tests/test_gpu_parity.py, bench.py --config cfg5h).
+//
+// Term h[k]*x[i-k] of the output at image index i, grouped by fp16 pair
+// W = (x[2W], x[2W+1]): d = i - 2W, pair taps (h[d], h[d-1]) with h[-1] =
+// h[T] = 0 -- the table hp2[d], d = 0..T, packed half2 (lo, hi).
+namespace {
+
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+constexpr int kLongRH = 8;  // outputs per lane (keeps each lane's pair window 16-B aligned)
+
+struct LongHArgs {
+  const _Float16* x;
+  long long n, x_stride;       // in halves
+  const uint32_t* hp2;          // T+1 packed pairs, padded to a multiple of 32
+  int ntaps;
+  const _Float16* state;
+  int ns;
+  float* y;
+  long long y_stride;
+  int tiles_per_stream;
+  int halo;   // roundup8(ntaps): image halves before the first output
+  int img;    // image halves (multiple of 8)
+};
+
+__global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t imgw[];  // image as packed pairs
+  constexpr int R = kLongRH, NTH = 64 * kLongNW, KP = 32;  // KP tap pairs (d values) per pass
+  constexpr int OUT_WG = 64 * R * kLongNW;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int s = blockIdx.x / a.tiles_per_stream;
+  const int tile = blockIdx.x - s * a.tiles_per_stream;
+  const long long m0 = (long long)tile * OUT_WG;
+  const long long pb = m0 - a.halo;  // multiple of 8
+  const _Float16* xs = a.x + (long long)s * a.x_stride;
+  const _Float16* st = a.state + (long long)s * a.ns;
+  _Float16* imgh = reinterpret_cast<_Float16*>(imgw);
+  const int n8 = a.img >> 3;  // 16-B chunks
+  for (int c = tid; c < n8; c += NTH) {
+    const long long p = pb + 8LL * c;
+    if (p >= 0 && p + 8 <= a.n) {
+      *reinterpret_cast<uint4*>(imgh + 8 * c) = *reinterpret_cast<const uint4*>(xs + p);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const long long q = p + r;
+        imgh[8 * c + r] = q >= 0 ? (q < a.n ? xs[q] : (_Float16)0) : (q >= -a.ns ? st[a.ns + q] : (_Float16)0);
+      }
+    }
+  }
+  __syncthreads();
+
+  // output r of this lane: image half index i_r = I0 + r, I0 = lb + halo
+  const int lb = (wave * 64 + lane) * R;
+  const int I0 = lb + a.halo;                      // multiple of 8: pair index I0/2 16-B aligned
+  using hconst = const __attribute__((address_space(4))) uint32_t*;
+  const hconst hc = (hconst)a.hp2;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+  const int npass = (a.ntaps + 1 + KP - 1) / KP;  // d = 0..T
+  for (int P = 0; P < npass; ++P) {
+    uint32_t hs[KP];
+#pragma unroll
+    for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
+#pragma unroll
+    for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
+    // pair W for (r, d): 2W = I0 + r - d, d = KP*P + dd.  Word index
+    // W = I0/2 - KP*P/2 + (r - dd)/2 ranges over base + [-(KP/2), 1].
+    const int wbase = (I0 >> 1) - (KP / 2) * P - (KP / 2);  // word of relative index 0
+    // relative word u = (r - dd)/2 + KP/2 in [0, KP/2 + 1]; read 4-word chunks
+    constexpr int NU = KP / 2 + R / 2;  // u = (r - dd)/2 + KP/2 in [1, KP/2 + R/2 - 1]
+    constexpr int NC = (NU + 3) / 4;
+    // I0/2 and (KP/2)*(P+1) are multiples of 4: 16-B aligned chunks
+    const uint32_t* base = imgw + wbase;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + 4 * c);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = 4 * c + q;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int dd = r - 2 * (u - KP / 2);  // d - KP*P
+          if (dd >= 0 && dd < KP) {
+            half2_t xv = __builtin_bit_cast(half2_t, wv[q]);
+            half2_t hv = __builtin_bit_cast(half2_t, hs[dd]);
+            acc[r] = __builtin_amdgcn_fdot2(xv, hv, acc[r], false);
+          }
+        }
+      }
+    }
+  }
+  const long long m = m0 + lb;
+  float* ys = a.y + (long long)s * a.y_stride;
+  if (m + R <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
+    *reinterpret_cast<float4*>(ys + m) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(ys + m + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (m + r < a.n) ys[m + r] = acc[r];
+  }
+}
+
+// hp2[d] = (half(h[d]), half(h[d-1])) for d = 0..T, zero past both ends and
+// up to the padded length.
+__global__ __launch_bounds__(kWG) void build_pairs_h(const float* __restrict__ h, int ntaps, int len, uint32_t* hp2) {
+  const int d = blockIdx.x * kWG + threadIdx.x;
+  if (d >= len) return;
+  const _Float16 lo = d < ntaps ? (_Float16)h[d] : (_Float16)0;
+  const _Float16 hi = (d >= 1 && d - 1 < ntaps) ? (_Float16)h[d - 1] : (_Float16)0;
+  half2_t v = {lo, hi};
+  hp2[d] = __builtin_bit_cast(uint32_t, v);
+}
+
+__global__ __launch_bounds__(kWG) void long_commit_h(const _Float16* __restrict__ x, long long n,
+                                                     long long x_stride, _Float16* state, int ns) {
+  const int s = blockIdx.y;
+  const int i = blockIdx.x * kWG + threadIdx.x;
+  if (i >= ns) return;
+  state[(long long)s * ns + i] = x[(long long)s * x_stride + n - ns + i];
+}
+
+__global__ __launch_bounds__(kWG) void f32_to_f16(const float* __restrict__ x, long long count, _Float16* y) {
+  const long long i = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (i < count) y[i] = (_Float16)x[i];
+}
+
+}  // namespace
+
+size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32); }
+
+hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
+                             void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
+                             hipStream_t st) {
+  const int len = (int)fir_long_h_pairs(ntaps);
+  hipLaunchKernelGGL(build_pairs_h, dim3((len + kWG - 1) / kWG), dim3(kWG), 0, st, h, ntaps, len, scratch_pairs);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  LongHArgs a;
+  a.x = static_cast<const _Float16*>(x);
+  a.n = n;
+  a.x_stride = x_stride;
+  a.hp2 = scratch_pairs;
+  a.ntaps = ntaps;
+  a.state = static_cast<const _Float16*>(state);
+  a.ns = ns;
+  a.y = y;
+  a.y_stride = y_stride;
+  constexpr int OUT_WG = 64 * kLongRH * kLongNW;
+  a.tiles_per_stream = (int)((n + OUT_WG - 1) / OUT_WG);
+  a.halo = (ntaps + 7) / 8 * 8 + 32;  // covers d up to the padded pass end
+  a.img = a.halo + OUT_WG + 8;
+  const long long blocks = (long long)a.tiles_per_stream * nstreams;
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fir_long_h, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2, st, a);
+  e = hipGetLastError();
+  if (e != hipSuccess || ns <= 0) return e;
+  hipLaunchKernelGGL(long_commit_h, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st,
+                     static_cast<const _Float16*>(x), n, x_stride, static_cast<_Float16*>(state), ns);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_f16(const float* x, long long count, void* y, hipStream_t st) {
+  hipLaunchKernelGGL(f32_to_f16, dim3((unsigned)((count + kWG - 1) / kWG)), dim3(kWG), 0, st, x, count,
+                     static_cast<_Float16*>(y));
+  return hipGetLastError();
+}
+
 }  // namespace sdr

@@ -68,6 +68,14 @@ hipError_t launch_u8_to_planar(const uint8_t* iq, long long npairs, int nstreams
 // Long FIRs without decimation (fir_long.hip): T a multiple of 32.
 bool fir_long_ok(int D, int ntaps, int ns, long long n);
 hipError_t launch_fir_long(const FirLaunch& a, const float* h, hipStream_t st);
+// fp16-storage arm (not bit-exact; tolerance-tested): x/state are fp16
+// [nstreams][x_stride] / [nstreams][ns], y fp32; scratch_pairs holds
+// fir_long_h_pairs(ntaps) packed tap pairs.
+size_t fir_long_h_pairs(int ntaps);
+hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
+                             void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
+                             hipStream_t st);
+hipError_t launch_f32_to_f16(const float* x, long long count, void* y, hipStream_t st);
 
 // Whether the tiled fast path handles (D, ntaps, ns) for this source; false
 // means launch_fir takes the generic path (still exact, slower).

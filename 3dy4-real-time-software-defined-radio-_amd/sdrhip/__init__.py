@@ -72,6 +72,8 @@ _SIGS = {
     "sdr_frontend_f32_dev": [_vp, _i, _vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _ll],
     "sdr_frontend_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _ll],
     "sdr_resample_f32_dev": [_vp, _i, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_fir_block_f16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_f32_to_f16_dev": [_vp, _vp, _ll, _vp],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
 }
@@ -285,6 +287,14 @@ class Context:
     def resample_dev(self, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
         self._check(lib().sdr_resample_f32_dev(self._c, up, down, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
                                                _ptr(state), ns, _ptr(y), y_stride), "resample_dev")
+
+    def fir_block_f16_dev(self, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
+        """fp16-storage arm of blockConvolveFIR (tolerance, not bit-exact)."""
+        self._check(lib().sdr_fir_block_f16_dev(self._c, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
+                                                _ptr(state), ns, _ptr(y), y_stride), "fir_block_f16_dev")
+
+    def f32_to_f16_dev(self, x, count, y):
+        self._check(lib().sdr_f32_to_f16_dev(self._c, _ptr(x), count, _ptr(y)), "f32_to_f16_dev")
 
     def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
         self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")

@@ -50,6 +50,10 @@ CONFIGS = {
                  workload="fir101_dec10_fmdemod_f32_8streams_x32blocks_of_262150"),
     "cfg5": dict(kind="fir_block", D=1, ntaps=1024, n=1048576, streams=2,
                  workload="fir1024_block1M_f32_IandQ"),
+    # BASELINE config 5's fp16 arm: fp16 storage, fp32 accumulation (v_dot2_f32_f16); not
+    # bit-exact -- the line carries its error against the exact fp32 path
+    "cfg5h": dict(kind="fir_block_f16", D=1, ntaps=1024, n=1048576, streams=2,
+                  workload="fir1024_block1M_f16storage_IandQ"),
 }
 
 
@@ -176,13 +180,13 @@ def main():
     iq = torch.empty(S * 2 * n, dtype=torch.uint8, device=dev)
     ctx.synth_fm_u8_dev(iq, n, S, 2 * n, seed)
     kind = cfg["kind"]
-    if kind in ("frontend_f32", "fir_block", "resample"):
+    if kind in ("frontend_f32", "fir_block", "fir_block_f16", "resample"):
         I = torch.empty(S * n, dtype=torch.float32, device=dev)
         Q = torch.empty(S * n, dtype=torch.float32, device=dev)
         ctx.u8_to_planar_dev(iq, n, S, 2 * n, I, Q, n)
         torch.cuda.synchronize(dev)
         del iq
-    ns = {"resample": 150, "fir_block": T - 1}.get(kind, 100)
+    ns = {"resample": 150, "fir_block": T - 1, "fir_block_f16": T - 1}.get(kind, 100)
     st0 = torch.zeros(S * ns, dtype=torch.float32, device=dev)
     st1 = torch.zeros(S * ns, dtype=torch.float32, device=dev)
     p0 = torch.zeros(S, dtype=torch.float32, device=dev)
@@ -202,7 +206,10 @@ def main():
         flops_per_unit = 2 * 2 * T / D + 10
         unit = "MS/s"
         metric = "IQ MSamples/sec through FIR+decimate+FM-demod"
-        bound = "hbm"
+        # f32 planar input: 8.4 B against ~41 FLOP per pair -> HBM-bound; the u8
+        # wire format moves 2.4 B per pair, which puts the exact (no-FMA) FIR
+        # arithmetic above the ridge -> VALU-bound
+        bound = "hbm" if kind == "frontend_f32" else "valu"
     elif kind == "resample":
         up, down = cfg["up"], cfg["down"]
         ny = sdrhip.resample_out_len(up, down, n)
@@ -214,7 +221,7 @@ def main():
         unit = "MS/s"
         metric = "IF MSamples/sec (input) through the polyphase resampler"
         bound = "hbm"
-    else:  # fir_block, I and Q as two streams
+    elif kind == "fir_block":  # I and Q as two streams
         out = torch.empty(S * n, dtype=torch.float32, device=dev)
         IQ = torch.stack([I[:n], Q[:n]])
         step = lambda: ctx.fir_block_dev(IQ, n, 2, n, d_h, T, st0, ns, out, n)  # noqa: E731
@@ -224,6 +231,31 @@ def main():
         unit = "MS/s"
         metric = "IQ MSamples/sec through a 1024-tap FIR"
         bound = "valu"
+    else:  # fir_block_f16: fp16 storage of I and Q (converted once, untimed)
+        IQ = torch.stack([I[:n], Q[:n]])
+        IQh = torch.empty(2 * n, dtype=torch.float16, device=dev)
+        ctx.f32_to_f16_dev(IQ, 2 * n, IQh)
+        sth = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
+        out = torch.empty(2 * n, dtype=torch.float32, device=dev)
+        step = lambda: ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, sth, ns, out, n)  # noqa: E731
+        units = n
+        bytes_per_pair = 2.0 * 2 + 8.0  # fp16 in, fp32 out
+        flops_per_unit = 2.0 * 2 * T
+        unit = "MS/s"
+        metric = "IQ MSamples/sec through a 1024-tap FIR"
+        bound = "valu"
+        # error of this arm against the exact fp32 path on the same first block
+        ref = torch.empty(2 * n, dtype=torch.float32, device=dev)
+        z32 = torch.zeros(2 * ns, dtype=torch.float32, device=dev)
+        ctx.fir_block_dev(IQ, n, 2, n, d_h, T, z32, ns, ref, n)
+        z16 = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
+        got = torch.empty(2 * n, dtype=torch.float32, device=dev)
+        ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, z16, ns, got, n)
+        torch.cuda.synchronize(dev)
+        err = float((got - ref).abs().max())
+        scale = float(d_h.abs().sum()) * float(IQ.abs().max())
+        tolerance = {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale,
+                     "norm": "sum|h| * max|x|", "rms_err": float((got - ref).pow(2).mean().sqrt())}
 
     for _ in range(args.warmup):
         step()
@@ -258,8 +290,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4)}
     else:
         achieved = units * flops_per_unit / launch_s / 1e12
-        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_VALU_PEAK_TFLOPS, 4)}
+        # fp16 arm: v_dot2_f32_f16 retires two products per lane per issue -> twice the fp32 vector peak
+        peak = FP32_VALU_PEAK_TFLOPS * (2 if kind == "fir_block_f16" else 1)
+        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4)}
     traffic = None
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):
@@ -270,6 +304,8 @@ def main():
     roof["traffic"] = traffic
     roof["algorithmic_bytes_per_launch"] = int(units * bytes_per_pair)
 
+    if kind != "fir_block_f16":
+        tolerance = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("cfg2", "cfg2u8", "cfg4"):
         cpu = cpu_baseline(args.cpu_seconds)
@@ -277,11 +313,13 @@ def main():
         line = {
             "metric": metric, "value": round(value, 1), "unit": unit, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16" if kind == "fir_block_f16" else "f32",
+            "data": "synthetic",
             "config": {"workload": cfg["workload"], "streams_per_gpu": S, "pairs_per_stream_per_step": n,
                        "ntaps": T, "parallelism": f"{world} GPU(s) x independent streams, no data-path collective",
                        "state_carried_across_steps": True},
             "roofline": roof, "cpu_baseline": cpu,
+            **({"tolerance": tolerance} if tolerance else {}),
             "wall_ms": round(ms_wall, 3),
         }
         print(json.dumps(line), flush=True)

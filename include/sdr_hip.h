@@ -134,6 +134,17 @@ int sdr_resample_f32_dev(sdr_ctx *ctx, int up, int down, const float *x, long lo
                          long long x_stride, const float *h, int ntaps, float *state, int ns, float *y,
                          long long y_stride);
 
+/* BASELINE config 5's fp16 arm of blockConvolveFIR (src/filter.cpp:66-83):
+ * x and state are fp16 (IEEE binary16, [nstreams][x_stride] / [nstreams][ns]),
+ * taps fp32 (rounded to fp16 inside), y fp32.  fp32 accumulation of fp16
+ * products (v_dot2_f32_f16).  NOT bit-exact with the reference -- a
+ * tolerance arm; the fp32 calls above are the exact path.  Rows must be
+ * 16-B aligned. */
+int sdr_fir_block_f16_dev(sdr_ctx *ctx, const void *x, long long n, int nstreams, long long x_stride,
+                          const float *h, int ntaps, void *state, int ns, float *y, long long y_stride);
+/* fp32 -> fp16 (round to nearest even), count elements, stream-ordered. */
+int sdr_f32_to_f16_dev(sdr_ctx *ctx, const float *x, long long count, void *y);
+
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the
  * device (counter-based, keyed by (seed, stream, sample)); used by the

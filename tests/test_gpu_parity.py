@@ -177,6 +177,42 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, n
         assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
 
 
+@pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000)])
+def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, ntaps, n):
+    """BASELINE config 5's fp16 arm (fp16 storage, fp32 dot2 accumulation):
+    within 2^-9 * sum|h| * max|x| of the exact fp32 reference, and within
+    fp32 accumulation error of the exact sum over the fp16-rounded operands.
+    The carried fp16 state is the last ns inputs, exactly."""
+    sdrhip = built_lib
+    rng = np.random.default_rng(ntaps + n)
+    h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
+    ns, nstreams = ntaps - 1, 2
+    st_ref = [np.zeros(ns, np.float32) for _ in range(nstreams)]
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    sth = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(nstreams * ns, np.float16))
+    y = sdrhip.DeviceArray(gpu_ctx, nstreams * n * 4)
+    hh = h.astype(np.float16).astype(np.float64)
+    prev16 = [np.zeros(ns, np.float64) for _ in range(nstreams)]
+    for blk in range(2):
+        x = rng.standard_normal((nstreams, n)).astype(np.float32)
+        xh = sdrhip.DeviceArray.from_numpy(gpu_ctx, x.astype(np.float16))
+        gpu_ctx.fir_block_f16_dev(xh, n, nstreams, n, d_h, ntaps, sth, ns, y, n)
+        gpu_ctx.synchronize()
+        got = y.download().reshape(nstreams, n)
+        for s in range(nstreams):
+            want = oracle.fir_block(x[s], h, st_ref[s])
+            scale = np.abs(h).sum() * np.abs(x[s]).max()
+            assert np.abs(got[s] - want).max() <= 2.0 ** -9 * scale, f"stream {s} block {blk} vs fp32"
+            # exact sum over the fp16-rounded operands (fp64), fp32 accumulation bound
+            xs = np.concatenate([prev16[s], x[s].astype(np.float16).astype(np.float64)])
+            exact = np.convolve(xs, hh)[ns:ns + n]
+            bound = ntaps * 2.0 ** -23 * np.convolve(np.abs(xs), np.abs(hh))[ns:ns + n] + 1e-30
+            assert np.all(np.abs(got[s] - exact) <= bound), f"stream {s} block {blk} vs fp16-operand sum"
+            prev16[s] = xs[-ns:]
+        assert np.array_equal(sth.download(np.float16).reshape(nstreams, ns),
+                              x[:, -ns:].astype(np.float16)), "fp16 state"
+
+
 # ------------------------------------------------------- batched device API
 
 def _fm_streams(nstreams, n, seed=5):
