@@ -95,51 +95,38 @@ __global__ __launch_bounds__(kWG) void resample_tile(const float* __restrict__ x
 // ds_read_b128 never share a bank.
 constexpr int kPPLanes = 64;
 
-template <int CMAX, int A, int I0, int I1>
-__device__ __forceinline__ void pp_pass(float& acc, const float* wl, int ctop, const float* hs) {
-  // element of tap i: LDS index 4*(ctop - cc) + jj with i = 4*cc + A - jj
-  constexpr int CLO = (I0 - A) > 0 ? (I0 - A + 3) / 4 : 0;
-  constexpr int CHI = (I1 + 2 - A) / 4;
-  float4 q = *reinterpret_cast<const float4*>(wl + 4 * (ctop - CLO));
+// Taps come from this wave's LDS tap row, pre-shifted by the wave's
+// alignment A so that chunk cc's four taps are one aligned float4:
+// trow[4*cc + 3 - jj] = tap i = 4*cc + A - jj.  All lanes read the same
+// address (a broadcast); the window chunk is this lane's own.
+template <int CMAX, int A>
+__device__ __forceinline__ float pp_scan(const float* wl, int ctop, const float* trow) {
+  constexpr int CHI = (CMAX - 1 + 3 - A) / 4;  // last chunk holding a tap
+  constexpr int PD = 4;                        // chunks in flight ahead of the one consumed
+  const float* lo = wl + 4 * (ctop - CHI);     // window chunk cc at lo + 4*(CHI - cc)
+  float acc = 0.0f;
+  float4 q[CHI + 1], t[CHI + 1];               // compile-time indexed: a register ring
 #pragma unroll
-  for (int cc = CLO; cc <= CHI; ++cc) {
-    float4 nx = q;
-    if (cc < CHI) nx = *reinterpret_cast<const float4*>(wl + 4 * (ctop - cc - 1));
-    const float e[4] = {q.x, q.y, q.z, q.w};
+  for (int cc = 0; cc < PD && cc <= CHI; ++cc) {
+    q[cc] = *reinterpret_cast<const float4*>(lo + 4 * (CHI - cc));
+    t[cc] = *reinterpret_cast<const float4*>(trow + 4 * cc);
+  }
+#pragma unroll
+  for (int cc = 0; cc <= CHI; ++cc) {
+    if (cc + PD <= CHI) {
+      q[cc + PD] = *reinterpret_cast<const float4*>(lo + 4 * (CHI - cc - PD));
+      t[cc + PD] = *reinterpret_cast<const float4*>(trow + 4 * (cc + PD));
+    }
+    const float e[4] = {q[cc].x, q[cc].y, q[cc].z, q[cc].w};
+    const float hv[4] = {t[cc].w, t[cc].z, t[cc].y, t[cc].x};  // hv[jj] = tap 4*cc + A - jj
 #pragma unroll
     for (int jj = 3; jj >= 0; --jj) {
       const int i = 4 * cc + A - jj;
-      if (i >= I0 && i < I1) acc = acc + hs[i - I0] * e[jj];
+      if (i >= 0 && i < CMAX) acc = acc + hv[jj] * e[jj];
     }
-    q = nx;
     asm volatile("" : "+v"(acc));
     __builtin_amdgcn_sched_barrier(0);
   }
-}
-
-template <int CMAX, int A>
-__device__ __forceinline__ float pp_scan(const float* wl, int ctop, const float* __restrict__ hrow) {
-  constexpr int KP = 32;
-  using hconst = const __attribute__((address_space(4))) float*;
-  const hconst hc = (hconst)hrow;
-  float acc = 0.0f;
-  float hs[KP];
-  auto pass = [&](auto i0c) {
-    constexpr int I0 = decltype(i0c)::value;
-    constexpr int I1 = I0 + KP < CMAX ? I0 + KP : CMAX;
-#pragma unroll
-    for (int i = 0; i < I1 - I0; ++i) hs[i] = hc[I0 + i];
-#pragma unroll
-    for (int i = 0; i < I1 - I0; ++i) asm volatile("" : "+s"(hs[i]));
-    pp_pass<CMAX, A, I0, I1>(acc, wl, ctop, hs);
-  };
-  pass(std::integral_constant<int, 0>{});
-  if constexpr (CMAX > KP) pass(std::integral_constant<int, KP>{});
-  if constexpr (CMAX > 2 * KP) pass(std::integral_constant<int, 2 * KP>{});
-  if constexpr (CMAX > 3 * KP) pass(std::integral_constant<int, 3 * KP>{});
-  if constexpr (CMAX > 4 * KP) pass(std::integral_constant<int, 4 * KP>{});
-  if constexpr (CMAX > 5 * KP) pass(std::integral_constant<int, 5 * KP>{});
-  static_assert(CMAX <= 6 * KP, "more tap passes");
   return acc;
 }
 
@@ -212,6 +199,8 @@ template <int CMAX>
 __global__ __launch_bounds__(1024, 1) void resample_pp(PPArgs a) {
   __shared__ __attribute__((aligned(16))) float imgA[kPPLanes * kPPSeg];
   __shared__ __attribute__((aligned(16))) float imgB[kPPLanes * kPPSeg];
+  constexpr int TROW = ((CMAX + 3 + 3) / 4) * 4;  // floats per wave tap row
+  __shared__ __attribute__((aligned(16))) float taps[16 * TROW];
   const int nw = blockDim.x >> 6;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   const int grp = blockIdx.x % a.nphg;
@@ -235,20 +224,32 @@ __global__ __launch_bounds__(1024, 1) void resample_pp(PPArgs a) {
   const int off = (int)(((long long)phi * a.down) / a.up - q0);
   const int e1 = off + CMAX - 1 + sa;  // segment element of tap i = 0 (newest input)
   const int A = e1 & 3, ctop = e1 >> 2;
-  const float* hrow = a.hp + (long long)(wave_on ? p : 0) * a.cpad;
+  // this wave's tap row, shifted by A (fixed for the workgroup's lifetime)
+  float* trow = taps + wv * TROW;
+  {
+    const float* hrow = a.hp + (long long)(wave_on ? p : 0) * a.cpad;
+    for (int u = ln; u < TROW; u += 64) {
+      const int i = u + A - 3;
+      trow[u] = (i >= 0 && i < CMAX) ? hrow[i] : 0.0f;
+    }
+  }
 
   auto compute = [&](long long cb, const float* img) __attribute__((always_inline)) {
     if (!wave_on || a.ablate == 2) return;
     const long long col = cb * kPPLanes + ln;
     const long long sidx = col / a.np, t = col - sidx * a.np;
     const long long j = (long long)a.up * t + phi;
-    const float* wl = img + ln * a.segpad;
+    // opaque per tile: keeps the chunk addresses from being hoisted out of
+    // the tile loop into one VGPR each
+    int woff = ln * a.segpad + 4 * ctop;
+    asm volatile("" : "+v"(woff));
+    const float* wl = img + woff;
     float acc;
     switch (A) {  // wave-uniform
-      case 0: acc = pp_scan<CMAX, 0>(wl, ctop, hrow); break;
-      case 1: acc = pp_scan<CMAX, 1>(wl, ctop, hrow); break;
-      case 2: acc = pp_scan<CMAX, 2>(wl, ctop, hrow); break;
-      default: acc = pp_scan<CMAX, 3>(wl, ctop, hrow); break;
+      case 0: acc = pp_scan<CMAX, 0>(wl, 0, trow); break;
+      case 1: acc = pp_scan<CMAX, 1>(wl, 0, trow); break;
+      case 2: acc = pp_scan<CMAX, 2>(wl, 0, trow); break;
+      default: acc = pp_scan<CMAX, 3>(wl, 0, trow); break;
     }
     if (col < a.ncols && j < a.ny) a.y[sidx * a.y_stride + j] = acc;
   };
