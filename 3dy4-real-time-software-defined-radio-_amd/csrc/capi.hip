@@ -18,14 +18,14 @@ struct sdr_ctx {
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
   // grow-only device scratch for the host-pointer wrappers and internal use
-  void* buf[10] = {};
-  size_t cap[10] = {};
+  void* buf[13] = {};
+  size_t cap[13] = {};
   std::string err;
 };
 
 namespace {
 
-enum Slot { kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp };
+enum Slot { kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp, kPipe0, kPipe1, kPipe2 };
 
 int fail(sdr_ctx* c, int code, const char* fmt, ...) {
   if (c) {
@@ -419,6 +419,60 @@ int sdr_f32_to_f16_dev(sdr_ctx* c, const float* x, long long count, void* y) {
   hipError_t e = sdr::launch_f32_to_f16(x, count, y, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "f32_to_f16 launch");
   return SDR_OK;
+}
+
+int sdr_delay_f32_dev(sdr_ctx* c, const float* in, long long n, int nstreams, long long in_stride, float* state,
+                      int ns, float* out, long long out_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!in || !state || !out) return fail(c, SDR_EINVAL, "null pointer");
+  if (n <= 0 || nstreams < 1 || ns < 0) return fail(c, SDR_EINVAL, "empty block / bad sizes");
+  if (n < ns) return fail(c, SDR_EINVAL, "block length %lld < delay %d (filter.cpp delayBlock reads past the block)", n,
+                          ns);
+  if (ns > 256) return fail(c, SDR_EINVAL, "delay %d > 256 not supported on the device path", ns);
+  if (nstreams > 1 && (in_stride < n || out_stride < n)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  hipError_t e = sdr::launch_delay(in, n, nstreams, in_stride, state, ns, out, out_stride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "delay launch");
+  return SDR_OK;
+}
+
+int sdr_pcm_s16_dev(sdr_ctx* c, const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
+                    long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!x || !pcm || n < 0 || nstreams < 1) return fail(c, SDR_EINVAL, "bad pcm arguments");
+  if (n == 0) return SDR_OK;
+  hipError_t e = sdr::launch_pcm(x, n, nstreams, x_stride, pcm, pcm_stride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "pcm launch");
+  return SDR_OK;
+}
+
+int sdr_mono_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
+                        const float* h_rf, int rf_taps, float* state_i, float* state_q, int ns_rf, float* prev_i,
+                        float* prev_q, float* delay_state, int ns_delay, int up, int down, const float* h_audio,
+                        int audio_taps, float* state_audio, int ns_audio, int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (D < 1 || npairs <= 0 || npairs % D) return fail(c, SDR_EINVAL, "block of %lld pairs is not a multiple of %d",
+                                                   npairs, D);
+  const long long nd = npairs / D;  // demodulated samples per stream
+  const long long na = sdr_resample_out_len(up, down, nd);
+  if (na <= 0) return fail(c, SDR_EINVAL, "empty audio block");
+  if (nstreams > 1 && pcm_stride < na) return fail(c, SDR_EINVAL, "pcm stride < audio samples per block");
+  // rows of the intermediate buffers: multiples of 4 floats (16-B aligned rows for the tiled kernels)
+  const long long dstride = (nd + 3) / 4 * 4, astride = (na + 3) / 4 * 4;
+  float* demod = static_cast<float*>(scratch(c, kPipe0, (size_t)nstreams * dstride * sizeof(float)));
+  float* delayed = static_cast<float*>(scratch(c, kPipe1, (size_t)nstreams * dstride * sizeof(float)));
+  float* audio = static_cast<float*>(scratch(c, kPipe2, (size_t)nstreams * astride * sizeof(float)));
+  if (!demod || !delayed || !audio) return fail(c, SDR_ENOMEM, "pipeline buffers");
+  if ((rc = sdr_frontend_u8_dev(c, D, iq, npairs, nstreams, iq_stride, h_rf, rf_taps, state_i, state_q, ns_rf, prev_i,
+                                prev_q, demod, dstride)))
+    return rc;
+  if ((rc = sdr_delay_f32_dev(c, demod, nd, nstreams, dstride, delay_state, ns_delay, delayed, dstride))) return rc;
+  if ((rc = sdr_resample_f32_dev(c, up, down, delayed, nd, nstreams, dstride, h_audio, audio_taps, state_audio,
+                                 ns_audio, audio, astride)))
+    return rc;
+  return sdr_pcm_s16_dev(c, audio, na, nstreams, astride, pcm, pcm_stride);
 }
 
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

@@ -1,0 +1,64 @@
+// pipeline.hip -- the device-resident mono back end around the front end
+// (SURVEY.md section 8(f) rows 2 and 4): delayBlock (src/filter.cpp:230-238
+// as src/project.cpp:114 uses it) and the s16 output stage of
+// src/project.cpp:311-314, batched over streams.  The audio resampler
+// between them is resample.hip / fir_tile.hip.
+#include "sdr_common.hpp"
+
+namespace sdr {
+namespace {
+
+// out = state ++ in[0 .. n-ns), state <- in[n-ns .. n).  Only workgroup
+// (0, s) reads state[s]; it rewrites it after a barrier, so one launch.
+__global__ __launch_bounds__(kWG) void delay_kernel(const float* __restrict__ in, long long n, long long in_stride,
+                                                    float* state, int ns, float* __restrict__ out,
+                                                    long long out_stride) {
+  const int s = blockIdx.y;
+  const float* x = in + (long long)s * in_stride;
+  float* y = out + (long long)s * out_stride;
+  float* st = state + (long long)s * ns;
+  for (long long i = (long long)blockIdx.x * kWG + threadIdx.x; i < n; i += (long long)gridDim.x * kWG)
+    y[i] = i < ns ? st[i] : x[i - ns];
+  if (blockIdx.x == 0) {
+    __syncthreads();  // every read of the old state in this workgroup is done
+    for (int j = threadIdx.x; j < ns; j += kWG) st[j] = x[n - ns + j];
+  }
+}
+
+// src/project.cpp:311-314: NaN -> 0, else static_cast<short>(x * 16384) as
+// the reference's compiler emits it (truncate to int32, keep the low 16
+// bits; values outside int32 give INT_MIN -> 0).
+__global__ __launch_bounds__(kWG) void pcm_kernel(const float* __restrict__ x, long long n, long long x_stride,
+                                                  int16_t* __restrict__ pcm, long long pcm_stride) {
+  const int s = blockIdx.y;
+  const long long i = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (i >= n) return;
+  const float u = x[(long long)s * x_stride + i];
+  int16_t r = 0;
+  if (!__builtin_isnan(u)) {
+    const float v = u * 16384.0f;
+    const int w = (v < 2147483648.0f && v >= -2147483648.0f) ? (int)v : (int)0x80000000u;
+    r = (int16_t)(uint16_t)((unsigned)w & 0xffffu);
+  }
+  pcm[(long long)s * pcm_stride + i] = r;
+}
+
+}  // namespace
+
+hipError_t launch_delay(const float* in, long long n, int nstreams, long long in_stride, float* state, int ns,
+                        float* out, long long out_stride, hipStream_t st) {
+  long long gx = (n + kWG - 1) / kWG;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(delay_kernel, dim3((unsigned)gx, (unsigned)nstreams), dim3(kWG), 0, st, in, n, in_stride, state,
+                     ns, out, out_stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
+                      long long pcm_stride, hipStream_t st) {
+  hipLaunchKernelGGL(pcm_kernel, dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0, st, x, n,
+                     x_stride, pcm, pcm_stride);
+  return hipGetLastError();
+}
+
+}  // namespace sdr

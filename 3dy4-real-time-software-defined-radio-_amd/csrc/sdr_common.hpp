@@ -60,6 +60,10 @@ hipError_t launch_demod(const float* I, const float* Q, long long n, int nstream
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
                            long long ny, float* scratch_taps, hipStream_t st);
+hipError_t launch_delay(const float* in, long long n, int nstreams, long long in_stride, float* state, int ns,
+                        float* out, long long out_stride, hipStream_t st);
+hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
+                      long long pcm_stride, hipStream_t st);
 hipError_t launch_synth_fm_u8(uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
                               unsigned long long seed, hipStream_t st);
 hipError_t launch_u8_to_planar(const uint8_t* iq, long long npairs, int nstreams, long long iq_stride, float* I,

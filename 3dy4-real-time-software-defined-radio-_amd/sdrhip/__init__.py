@@ -74,6 +74,10 @@ _SIGS = {
     "sdr_resample_f32_dev": [_vp, _i, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
     "sdr_fir_block_f16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
     "sdr_f32_to_f16_dev": [_vp, _vp, _ll, _vp],
+    "sdr_delay_f32_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
+    "sdr_pcm_s16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _ll],
+    "sdr_mono_pcm_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _i,
+                            _vp, _i, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
 }
@@ -295,6 +299,22 @@ class Context:
 
     def f32_to_f16_dev(self, x, count, y):
         self._check(lib().sdr_f32_to_f16_dev(self._c, _ptr(x), count, _ptr(y)), "f32_to_f16_dev")
+
+    def delay_dev(self, x, n, nstreams, x_stride, state, ns, y, y_stride):
+        self._check(lib().sdr_delay_f32_dev(self._c, _ptr(x), n, nstreams, x_stride, _ptr(state), ns, _ptr(y),
+                                            y_stride), "delay_dev")
+
+    def pcm_s16_dev(self, x, n, nstreams, x_stride, pcm, pcm_stride):
+        self._check(lib().sdr_pcm_s16_dev(self._c, _ptr(x), n, nstreams, x_stride, _ptr(pcm), pcm_stride),
+                    "pcm_s16_dev")
+
+    def mono_pcm_u8_dev(self, D, iq, npairs, nstreams, iq_stride, h_rf, rf_taps, st_i, st_q, ns_rf, prev_i, prev_q,
+                        delay_state, ns_delay, up, down, h_audio, audio_taps, st_audio, ns_audio, pcm, pcm_stride):
+        """src/project.cpp's mono path for one block of every stream: u8 IQ -> s16 PCM, on the device."""
+        self._check(lib().sdr_mono_pcm_u8_dev(self._c, D, _ptr(iq), npairs, nstreams, iq_stride, _ptr(h_rf), rf_taps,
+                                              _ptr(st_i), _ptr(st_q), ns_rf, _ptr(prev_i), _ptr(prev_q),
+                                              _ptr(delay_state), ns_delay, up, down, _ptr(h_audio), audio_taps,
+                                              _ptr(st_audio), ns_audio, _ptr(pcm), pcm_stride), "mono_pcm_u8_dev")
 
     def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
         self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")

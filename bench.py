@@ -50,6 +50,10 @@ CONFIGS = {
                  workload="fir101_dec10_fmdemod_f32_8streams_x32blocks_of_262150"),
     "cfg5": dict(kind="fir_block", D=1, ntaps=1024, n=1048576, streams=2,
                  workload="fir1024_block1M_f32_IandQ"),
+    # SURVEY 8(f) 2+4: the reference program's whole mono path (mode 0) on the device,
+    # u8 IQ -> front end -> delay -> audio FIR+dec5 -> s16 PCM, 51,200-pair reference blocks
+    "mono0": dict(kind="mono_u8", D=10, up=1, down=5, ntaps=101, n=51200, streams=1024,
+                  workload="mode0_mono_u8iq_to_s16pcm_block51200"),
     # BASELINE config 5's fp16 arm: fp16 storage, fp32 accumulation (v_dot2_f32_f16); not
     # bit-exact -- the line carries its error against the exact fp32 path
     "cfg5h": dict(kind="fir_block_f16", D=1, ntaps=1024, n=1048576, streams=2,
@@ -174,6 +178,8 @@ def main():
         taps = sdrhip.taps_lpf(240e3 * 147, 16e3, T, 147)
     else:
         taps = sdrhip.taps_lpf(2.4e6, 100e3, T, 1)
+    if cfg["kind"] == "mono_u8":  # src/project.cpp:263-266: the audio LPF of mode 0
+        d_ha = torch.from_numpy(sdrhip.taps_lpf(240e3, 16e3, 101, 1)).to(dev)
     d_h = torch.from_numpy(taps).to(dev)
 
     # synthetic input generated on the device (no host traffic), then kept resident
@@ -192,7 +198,21 @@ def main():
     p0 = torch.zeros(S, dtype=torch.float32, device=dev)
     p1 = torch.zeros(S, dtype=torch.float32, device=dev)
 
-    if kind in ("frontend_f32", "frontend_u8"):
+    if kind == "mono_u8":
+        D, up, down = cfg["D"], cfg["up"], cfg["down"]
+        na = sdrhip.resample_out_len(up, down, n // D)
+        sd = torch.zeros(S * 50, dtype=torch.float32, device=dev)
+        sa = torch.zeros(S * 100, dtype=torch.float32, device=dev)
+        pcm = torch.empty(S * na, dtype=torch.int16, device=dev)
+        step = lambda: ctx.mono_pcm_u8_dev(D, iq, n, S, 2 * n, d_h, T, st0, st1, ns, p0, p1, sd, 50, up, down,  # noqa
+                                           d_ha, 101, sa, 100, pcm, na)
+        units = S * n
+        bytes_per_pair = 2.0 + 2.0 * na / n  # u8 IQ in, s16 PCM out (intermediates are algorithmically free)
+        flops_per_unit = 2 * 2 * T / D + 10 + 2.0 * 101 / (D * down) + 1
+        unit = "MS/s"
+        metric = "IQ MSamples/sec through the mode-0 mono path (u8 IQ -> s16 PCM)"
+        bound = "valu"
+    elif kind in ("frontend_f32", "frontend_u8"):
         D = cfg["D"]
         nout = n // D
         out = torch.empty(S * nout, dtype=torch.float32, device=dev)

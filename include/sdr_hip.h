@@ -145,6 +145,24 @@ int sdr_fir_block_f16_dev(sdr_ctx *ctx, const void *x, long long n, int nstreams
 /* fp32 -> fp16 (round to nearest even), count elements, stream-ordered. */
 int sdr_f32_to_f16_dev(sdr_ctx *ctx, const float *x, long long count, void *y);
 
+/* ------------------------------- device-resident mono back end (8(f)) -- */
+/* delayBlock (src/filter.cpp, as src/project.cpp:114 uses it), batched:
+ * out = state ++ in[0 .. n-ns), state <- in[n-ns .. n).  ns <= 256. */
+int sdr_delay_f32_dev(sdr_ctx *ctx, const float *in, long long n, int nstreams, long long in_stride, float *state,
+                      int ns, float *out, long long out_stride);
+/* The output stage of src/project.cpp:311-314: NaN -> 0, else
+ * (short)(x * 16384) with the reference build's x86-64 conversion. */
+int sdr_pcm_s16_dev(sdr_ctx *ctx, const float *x, long long n, int nstreams, long long x_stride, int16_t *pcm,
+                    long long pcm_stride);
+/* The whole mono path of src/project.cpp:72-118 + 304-314 for one block of
+ * every stream, device-resident: u8 IQ -> fused front end -> delay ->
+ * audio resampler (up/down; up == 1 is FIR + decimate) -> s16 PCM.
+ * Bit-identical to the reference program's output (tests). */
+int sdr_mono_pcm_u8_dev(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs, int nstreams, long long iq_stride,
+                        const float *h_rf, int rf_taps, float *state_i, float *state_q, int ns_rf, float *prev_i,
+                        float *prev_q, float *delay_state, int ns_delay, int up, int down, const float *h_audio,
+                        int audio_taps, float *state_audio, int ns_audio, int16_t *pcm, long long pcm_stride);
+
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the
  * device (counter-based, keyed by (seed, stream, sample)); used by the

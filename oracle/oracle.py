@@ -182,6 +182,7 @@ class Oracle(_Lib):
         super().__init__(path)
         self.lib.or_resample_len.restype = _L
         self.lib.or_u8_to_planar.restype = _L
+        self.lib.or_pcm_s16.restype = _L
 
     def resample_len(self, up, down, nx):
         return int(self.lib.or_resample_len(C.c_int(up), C.c_int(down), _L(nx)))
@@ -193,6 +194,21 @@ class Oracle(_Lib):
         Q = np.zeros(n, np.float32)
         self.lib.or_u8_to_planar(iq.ctypes.data_as(_u8p), _L(n), _p(I), _p(Q))
         return I, Q
+
+    def pcm_s16(self, x):
+        """src/project.cpp:311-314: NaN -> 0, else (short)(x * 16384)."""
+        x = _f32(x)
+        out = np.zeros(max(len(x), 1), np.int16)
+        self._fn("pcm_s16")(_p(x), _L(len(x)), out.ctypes.data_as(C.c_void_p))
+        return out[:len(x)]
+
+    def mono(self, D, iq, h_rf, st_i, st_q, prev, delay_state, up, down, h_audio, st_audio):
+        """src/project.cpp:72-118 + 304-314 for one mono block: u8 IQ -> s16 PCM."""
+        I, Q = self.u8_to_planar(iq)
+        demod = self.frontend(D, I, Q, h_rf, st_i, st_q, prev)
+        delayed = self.delay_block(demod, delay_state)
+        audio = self.resample(up, down, delayed, h_audio, st_audio)
+        return self.pcm_s16(audio)
 
 
 class Reference(_Lib):

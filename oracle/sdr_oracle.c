@@ -284,6 +284,24 @@ long or_interleave(const float *l, long nl, const float *r, long nr, float *out)
     return n;
 }
 
+/* src/project.cpp:311-314, the output stage: NaN -> 0, else
+ * static_cast<short int>(x * 16384) (float product; the cast as the
+ * reference's compiler emits it on x86-64: truncate to int32, keep the low
+ * 16 bits; out-of-int32-range values give INT_MIN, i.e. 0). */
+long or_pcm_s16(const float *x, long n, short *out)
+{
+    for (long k = 0; k < n; k++) {
+        if (isnan(x[k])) {
+            out[k] = 0;
+        } else {
+            const float v = x[k] * 16384;
+            const int i = (v < 2147483648.0f && v >= -2147483648.0f) ? (int)v : (int)0x80000000u;
+            out[k] = (short)(unsigned short)((unsigned)i & 0xffffu);
+        }
+    }
+    return n;
+}
+
 /* ------------------------------------------------------- ingest + front -- */
 
 /* src/iofunc.cpp:117-119: float(((unsigned char)u - 128) / 128.0), then the

@@ -59,6 +59,8 @@ long or_pointwise_add(const float *a, long na, const float *b, long nb, float *o
 long or_pointwise_sub(const float *a, long na, const float *b, long nb, float *out);
 /* src/filter.cpp:291-301 */
 long or_interleave(const float *l, long nl, const float *r, long nr, float *out);
+/* src/project.cpp:311-314: float -> s16 PCM (NaN -> 0, x*16384 truncated) */
+long or_pcm_s16(const float *x, long n, short *out);
 
 /* src/iofunc.cpp:113-119 + src/project.cpp:78-81: u8 interleaved IQ -> planar float */
 long or_u8_to_planar(const unsigned char *iq, long npairs, float *I, float *Q);

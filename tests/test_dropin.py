@@ -117,3 +117,87 @@ def test_reference_project_on_dropin(gpu_ctx, mode, channel):
     out_hip = _project(hip, mode, channel, data)
     assert len(out_ref) > 0
     assert out_hip == out_ref
+
+
+# ------------------------------------------------- mono path, end to end
+
+MODES = {  # src/project.cpp:198-238: rf_Fs, rf_decim, audio_Fs, up, down, block bytes
+    0: (2.4e6, 10, 240e3, 1, 5, 102400),
+    1: (1.44e6, 5, 288e3, 1, 8, 81920),
+    2: (2.4e6, 10, 240e3, 147, 800, 160000),
+    3: (1.92e6, 5, 384e3, 147, 1280, 128000),
+}
+
+
+def _mono_setup(oracle, mode):
+    rf_fs, D, audio_fs, up, down, block_bytes = MODES[mode]
+    h_rf = oracle.taps_lpf(rf_fs, 100e3, 101, 1)
+    h_audio = oracle.taps_lpf(audio_fs * up, 16e3, 101 * up, up)
+    return rf_fs, D, up, down, block_bytes, h_rf, h_audio
+
+
+def _oracle_mono_stream(oracle, mode, data, nblocks):
+    """src/project.cpp's mono loop restated with the oracle, block by block."""
+    _, D, up, down, block_bytes, h_rf, h_audio = _mono_setup(oracle, mode)
+    st = dict(i=np.zeros(100, np.float32), q=np.zeros(100, np.float32), prev=np.zeros(2, np.float32),
+              delay=np.zeros(50, np.float32), audio=np.zeros(100, np.float32))
+    out = []
+    for b in range(nblocks):
+        iq = np.frombuffer(data[b * block_bytes:(b + 1) * block_bytes], np.uint8)
+        out.append(oracle.mono(D, iq, h_rf, st["i"], st["q"], st["prev"], st["delay"], up, down, h_audio,
+                               st["audio"]))
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_oracle_mono_chain_equals_reference_program(oracle, mode):
+    """Pins the oracle's mono chain (front end -> delay -> resampler -> s16,
+    src/project.cpp:72-118 + 304-314) to the reference program's own PCM
+    output (oracle/_ref/project_ref, built from the reference sources)."""
+    ref = os.path.join(REPO, "oracle", "_ref", "project_ref")
+    if not os.path.exists(ref):
+        pytest.skip("oracle/_ref/project_ref not built")
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, _, _, _, block_bytes, _, _ = _mono_setup(oracle, mode)
+    data = fm_iq_u8(block_bytes * 3 // 2, seed=70 + mode, fs=rf_fs).tobytes()
+    want = np.frombuffer(_project(ref, mode, "mono", data), np.int16)
+    got = _oracle_mono_stream(oracle, mode, data, 3)
+    assert len(want) == len(got) > 0
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode):
+    """sdr_mono_pcm_u8_dev: several independent streams x 3 blocks, u8 IQ in,
+    s16 PCM out, every byte equal to the oracle chain (itself pinned to the
+    reference program above); all carried state equal too."""
+    sdrhip = built_lib
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, D, up, down, block_bytes, h_rf, h_audio = _mono_setup(oracle, mode)
+    nstreams, nblk = 3, 3
+    npairs = block_bytes // 2
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    streams = [fm_iq_u8(npairs * nblk, seed=90 + 7 * s + mode, fs=rf_fs).tobytes() for s in range(nstreams)]
+    want = [_oracle_mono_stream(oracle, mode, streams[s], nblk) for s in range(nstreams)]
+    A = sdrhip.DeviceArray
+    d_hrf, d_ha = A.from_numpy(gpu_ctx, h_rf), A.from_numpy(gpu_ctx, h_audio)
+    z = lambda k: A.from_numpy(gpu_ctx, np.zeros(nstreams * k, np.float32))  # noqa: E731
+    si, sq, pi, pq, sd, sa = z(100), z(100), z(1), z(1), z(50), z(100)
+    pcm_stride = na + 5
+    d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
+    got = [[] for _ in range(nstreams)]
+    for b in range(nblk):
+        blk = np.stack([np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
+                        for s in range(nstreams)])
+        d_iq = A.from_numpy(gpu_ctx, np.ascontiguousarray(blk))
+        gpu_ctx.mono_pcm_u8_dev(D, d_iq, npairs, nstreams, block_bytes, d_hrf, len(h_rf), si, sq, 100, pi, pq,
+                                sd, 50, up, down, d_ha, len(h_audio), sa, 100, d_pcm, pcm_stride)
+        gpu_ctx.synchronize()
+        out = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :na]
+        for s in range(nstreams):
+            got[s].append(out[s].copy())
+    for s in range(nstreams):
+        assert np.array_equal(np.concatenate(got[s]), want[s]), f"stream {s}"
