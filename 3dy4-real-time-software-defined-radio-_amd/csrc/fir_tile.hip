@@ -150,24 +150,26 @@ __device__ __forceinline__ bool interior(const TileRef& tr, long long n) {
 // u8 coalesced vectors).  Chunk addresses are clamped into the block, so an
 // edge tile loads in-bounds but partly wrong data that edge_fill() then
 // overwrites.  No wait: stage_store consumes the registers.
-template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
-__device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int tid,
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC, bool CLAMP>
+__device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, int tid,
                                            float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
                                            float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   using G = Geom<D, T, R, DEMOD, NW>;
   auto load4 = [&](int i, float4& a0, float4& a1) {
-    const long long pmax = (n & ~3LL) - 4;  // last whole aligned chunk
     long long p = tr.pb + 4LL * i;
-    p = p < 0 ? 0 : (p > pmax ? pmax : p);
+    if constexpr (CLAMP) {
+      const long long pmax = (n & ~3LL) - 4;  // last whole aligned chunk
+      p = p < 0 ? 0 : (p > pmax ? pmax : p);
+    }
     if constexpr (SRC == Src::F32) {
       a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
       if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
     } else {
       const uint2 b = *reinterpret_cast<const uint2*>(tr.iq + 2 * p);
-      a0 = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu), u8_to_f32(b.y & 0xffu),
-                       u8_to_f32((b.y >> 16) & 0xffu));
-      a1 = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24), u8_to_f32((b.y >> 8) & 0xffu),
-                       u8_to_f32(b.y >> 24));
+      a0 = make_float4(u8_byte_to_f32<0>(b.x), u8_byte_to_f32<2>(b.x), u8_byte_to_f32<0>(b.y),
+                       u8_byte_to_f32<2>(b.y));
+      a1 = make_float4(u8_byte_to_f32<1>(b.x), u8_byte_to_f32<3>(b.x), u8_byte_to_f32<1>(b.y),
+                       u8_byte_to_f32<3>(b.y));
     }
   };
 #pragma unroll
@@ -175,6 +177,17 @@ __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int t
   // ragged last row: clamp the index (a redundant load) so every register
   // is defined and the arrays stay in VGPRs
   if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
+}
+
+// Clamped loads only where the span leaves the block (workgroup-uniform).
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int tid,
+                                           float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                           float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  if (tr.pb >= 0 && tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n)
+    stage_load_impl<D, T, R, DEMOD, NW, NCH, SRC, false>(tr, n, tid, v0, v1);
+  else
+    stage_load_impl<D, T, R, DEMOD, NW, NCH, SRC, true>(tr, n, tid, v0, v1);
 }
 
 // Edge tiles (a stream's first tile, and the one holding the chunk that

@@ -20,10 +20,10 @@ __global__ __launch_bounds__(kWG) void u8_to_planar(const uint8_t* __restrict__ 
   float* dq = Q + (long long)s * x_stride + g;
   if (g + 4 <= npairs) {
     const uint2 b = *reinterpret_cast<const uint2*>(src);
-    *reinterpret_cast<float4*>(di) = make_float4(u8_to_f32(b.x & 0xffu), u8_to_f32((b.x >> 16) & 0xffu),
-                                                 u8_to_f32(b.y & 0xffu), u8_to_f32((b.y >> 16) & 0xffu));
-    *reinterpret_cast<float4*>(dq) = make_float4(u8_to_f32((b.x >> 8) & 0xffu), u8_to_f32(b.x >> 24),
-                                                 u8_to_f32((b.y >> 8) & 0xffu), u8_to_f32(b.y >> 24));
+    *reinterpret_cast<float4*>(di) = make_float4(u8_byte_to_f32<0>(b.x), u8_byte_to_f32<2>(b.x),
+                                                 u8_byte_to_f32<0>(b.y), u8_byte_to_f32<2>(b.y));
+    *reinterpret_cast<float4*>(dq) = make_float4(u8_byte_to_f32<1>(b.x), u8_byte_to_f32<3>(b.x),
+                                                 u8_byte_to_f32<1>(b.y), u8_byte_to_f32<3>(b.y));
   } else {
     for (long long k = 0; g + k < npairs; ++k) {
       di[k] = u8_to_f32(src[2 * k]);

@@ -51,6 +51,14 @@ struct FirLaunch {
 // 2^-7 with |value| <= 1, so the float product below is the same number.
 __device__ __forceinline__ float u8_to_f32(uint32_t u) { return (float)((int)u - 128) * 0.0078125f; }
 
+// Byte b of a packed word, same value: v_cvt_f32_ubyte<b> then one fma --
+// u * 2^-7 - 1 is exact, so the single rounding of the fma changes nothing
+// (128 gives +0.0, as the reference's (u-128)/128.0 does).
+template <int B>
+__device__ __forceinline__ float u8_byte_to_f32(uint32_t w) {
+  return __builtin_fmaf((float)((w >> (8 * B)) & 0xffu), 0.0078125f, -1.0f);
+}
+
 // Host-side launchers, one per kernel family (defined next to the kernels).
 // allow_fast = false forces the generic kernel (misaligned buffers).
 hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, Src src, hipStream_t st,
