@@ -517,7 +517,9 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       float* o = a.out + (long long)tr.s * a.out_stride;
       // vector stores when the row keeps R-float groups aligned (uniform)
       const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
-      if (lane >= 1) {
+      // ablate 3 (timing only): no output stores unless the result is a
+      // value it never is, so the scan still runs
+      if (lane >= 1 && (a.ablate != 3 || d[0] == 12345.0f)) {
         if (vec && m0 + R <= nout) {
           if constexpr (R == 2) {
             *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);

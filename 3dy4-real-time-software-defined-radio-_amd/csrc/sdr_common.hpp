@@ -43,7 +43,7 @@ struct FirLaunch {
   int tiles_per_stream;
   int tiles_per_wg;  // persistent tile kernels: tiles per workgroup
   int walk;          // 0: each workgroup walks contiguous tiles; 1: XCD-strided (see fir_tile.hip)
-  int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math
+  int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math, 3 = no output stores
 };
 
 // Exact reference conversion of one wire byte, src/iofunc.cpp:118:
