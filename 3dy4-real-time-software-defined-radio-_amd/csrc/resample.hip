@@ -325,12 +325,25 @@ bool pp_enabled() {
 
 size_t resample_scratch_floats(int up, int ntaps) {
   const int cmax = (ntaps + up - 1) / up;
-  return (size_t)up * (size_t)((cmax + 3) / 4 * 4);
+  const size_t pp = (size_t)up * (size_t)((cmax + 3) / 4 * 4);
+  const size_t rs = resample_rs_scratch_floats(up, ntaps);
+  return pp > rs ? pp : rs;
 }
 
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
                            long long ny, float* scratch_taps, hipStream_t st) {
+  {
+    // the sliding-window kernel (resample_rs.hip) first, for the shapes it covers
+    hipError_t e = hipSuccess;
+    if (launch_resample_rs(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, scratch_taps,
+                           st, &e)) {
+      if (e != hipSuccess || ns <= 0) return e;
+      hipLaunchKernelGGL(resample_commit, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st, x, n,
+                         x_stride, state, ns);
+      return hipGetLastError();
+    }
+  }
   const int cmax = ((ntaps + up - 1) / up + 3) / 4 * 4;  // padded row length (16-B rows)
   const int tab = up * cmax;
   hipLaunchKernelGGL(build_polyphase, dim3((tab + kWG - 1) / kWG), dim3(kWG), 0, st, h, ntaps, up, cmax,

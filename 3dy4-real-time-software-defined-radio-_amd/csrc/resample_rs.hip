@@ -1,0 +1,358 @@
+// resample_rs.hip -- the polyphase resampler (src/filter.cpp:142-173) as a
+// sliding-window kernel: every input sample is staged in LDS about once.
+//
+// Decomposition (see resample.hip for the phase algebra): output
+// j = L*t + phi has phase p = (phi*M) mod L and newest input
+// q = t*M + floor(phi*M/L).  A *column* is one period t of one stream; a
+// workgroup owns 64 columns (lane = column) and walks ALL L phases of them
+// in groups of 32 (wave w takes phases 32g + w and 32g + 16 + w: two
+// independent accumulation chains per lane).  Consecutive phase groups need
+// windows that slide right by ~32*M/L inputs, so each column keeps a ring of
+// RING floats in LDS and only the new inputs of the next group are fetched
+// (LDS-DMA, one wave-instruction per column) while the current group is
+// computed.  Per-wave taps are SGPR operands read from a table pre-shifted
+// by the wave's window alignment A, so the chunk -> tap mapping is the same
+// for every A; the few out-of-range elements at the window ends are skipped
+// by uniform branches (the reference's sum has exactly CMAX terms).
+//
+// Arithmetic contract as everywhere: per output, k ascending (i = 0..CMAX-1),
+// separately rounded products and sums from 0.0f.
+#include <cstdlib>
+#include <type_traits>
+
+#include "sdr_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace sdr {
+namespace {
+
+constexpr int kRsLanes = 64;
+constexpr int kRsWaves = 16;
+constexpr int kRsPG = 2 * kRsWaves;  // phases per group
+constexpr int kRsRing = 512;         // floats per column ring (power of 2)
+constexpr int kRsRingC = kRsRing / 4;
+// column stride in LDS: one 16-B chunk of padding, so the 64 lanes' rings
+// (same ring offset, different columns) start on different banks
+constexpr int kRsColStride = kRsRing + 4;
+
+struct RsArgs {
+  const float* x;
+  long long n, x_stride;
+  const float* hs;  // [4][L][U] taps pre-shifted by A: hs[A][p][u] = tap u + A - 3
+  int U;            // row length (multiple of 4)
+  int up, down;
+  const float* state;
+  int ns;
+  float* y;
+  long long y_stride, ny;
+  int np;           // periods per stream
+  int ncols;        // nstreams * np
+  int ngrp;         // phase groups = ceil(up / kRsPG)
+  int ablate;
+};
+
+// Ring-relative coordinates: rel = (input position) - t*M - base0 with
+// base0 = -(CMAX-1) rounded down to a multiple of 4, so rel >= 0 for every
+// input any phase of the column reads; chunk c = rel/4 lives in ring slot
+// c mod (RING/4).
+
+// One DMA wave-instruction per (column, chunk range): chunks [c0, c1) of ring
+// coordinates (c = rel/4) of column cl.  Lanes past the range, and chunks that
+// reach outside [0, n), are skipped here and written in rs_edge().
+template <int CMAX>
+__device__ __forceinline__ void rs_dma(const RsArgs& a, float* ring, int cb, int wv, int ln, int base0,
+                                       int c0, int c1) {
+  for (int cl = wv; cl < kRsLanes; cl += kRsWaves) {
+    const int col = cb * kRsLanes + cl;
+    if (col >= a.ncols) break;
+    const int s = col / a.np, t = col - s * a.np;
+    const float* xs = a.x + (long long)s * a.x_stride;
+    float* col_ring = ring + cl * kRsColStride;
+    // pieces of <= 64 chunks that do not cross the ring's end: the LDS
+    // destination of lane k is always the (wave-uniform) base + 16*k
+    for (int p0 = c0; p0 < c1;) {
+      const int slot = p0 & (kRsRingC - 1);
+      int len = c1 - p0;
+      if (len > 64) len = 64;
+      if (len > kRsRingC - slot) len = kRsRingC - slot;
+      const long long g = (long long)t * a.down + base0 + 4 * (p0 + ln);  // input position of the chunk (multiple of 4)
+      if (ln < len && g >= 0 && g + 4 <= a.n)
+        __builtin_amdgcn_global_load_lds(xs + g, col_ring + 4 * slot, 16, 0, 0);
+      p0 += len;
+    }
+  }
+}
+
+template <int CMAX>
+__device__ __forceinline__ void rs_edge(const RsArgs& a, float* ring, int cb, int wv, int ln, int base0,
+                                        int c0, int c1) {
+  for (int cl = wv; cl < kRsLanes; cl += kRsWaves) {
+    const int col = cb * kRsLanes + cl;
+    if (col >= a.ncols) break;
+    const int s = col / a.np, t = col - s * a.np;
+    for (int c = c0 + ln; c < c1; c += 64) {
+      const long long g = (long long)t * a.down + base0 + 4LL * c;
+      if (!(g >= 0 && g + 4 <= a.n)) {
+        const float* xs = a.x + (long long)s * a.x_stride;
+        const float* st = a.state + (long long)s * a.ns;
+        float w4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long long gg = g + r;
+          w4[r] = gg >= 0 ? (gg < a.n ? xs[gg] : 0.0f) : (gg >= -a.ns ? st[a.ns + gg] : 0.0f);
+        }
+        *reinterpret_cast<float4*>(ring + cl * kRsColStride + 4 * (c & (kRsRingC - 1))) =
+            make_float4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    }
+  }
+}
+
+// Two phases of one wave over all shifted-tap chunks: element jj of chunk cc
+// is tap i = 4*cc + A - jj of its phase (uniform A per phase), at ring chunk
+// (ctop - cc) of the lane's ring; the four taps of chunk cc are one
+// broadcast ds_read_b128 of the phase's LDS tap row (hs row u = 4cc..4cc+3).
+template <int CMAX>
+__device__ __forceinline__ void rs_scan(float& acc0, float& acc1, const float* lr, int ctop0, int ctop1, int A0,
+                                        int A1, const float* t0row, const float* t1row) {
+  constexpr int NC = (CMAX + 3 + 3) / 4;  // shifted-tap chunks (u < CMAX + 3)
+  auto xchunk = [&](int ctop, int cc) {
+    return *reinterpret_cast<const float4*>(lr + 4 * ((ctop - cc) & (kRsRingC - 1)));
+  };
+  float4 x0 = xchunk(ctop0, 0), x1 = xchunk(ctop1, 0);
+  float4 h0 = *reinterpret_cast<const float4*>(t0row), h1 = *reinterpret_cast<const float4*>(t1row);
+#pragma unroll
+  for (int cc = 0; cc < NC; ++cc) {
+    float4 nx0 = x0, nx1 = x1, nh0 = h0, nh1 = h1;
+    if (cc + 1 < NC) {  // next chunk in flight while this one is multiplied
+      nx0 = xchunk(ctop0, cc + 1);
+      nx1 = xchunk(ctop1, cc + 1);
+      nh0 = *reinterpret_cast<const float4*>(t0row + 4 * (cc + 1));
+      nh1 = *reinterpret_cast<const float4*>(t1row + 4 * (cc + 1));
+    }
+    const float e0[4] = {x0.x, x0.y, x0.z, x0.w}, e1[4] = {x1.x, x1.y, x1.z, x1.w};
+    // shifted row: u = 4cc + 3 - jj, so element jj pairs with component 3 - jj
+    const float g0[4] = {h0.w, h0.z, h0.y, h0.x}, g1[4] = {h1.w, h1.z, h1.y, h1.x};
+#pragma unroll
+    for (int jj = 3; jj >= 0; --jj) {
+      // i = 4*cc + A - jj must lie in [0, CMAX): only the end chunks can miss.
+      // There the shifted tap is 0 and the ring element is replaced by 0, so
+      // the term is +0 and acc + 0 == acc exactly (acc starts at +0 and can
+      // never become -0): the sum keeps exactly the reference's CMAX terms,
+      // without branches.
+      float a0 = e0[jj], a1 = e1[jj];
+      if ((cc == 0) || (4 * cc + 3 - jj >= CMAX)) {
+        a0 = (4 * cc + A0 - jj >= 0 && 4 * cc + A0 - jj < CMAX) ? a0 : 0.0f;
+        a1 = (4 * cc + A1 - jj >= 0 && 4 * cc + A1 - jj < CMAX) ? a1 : 0.0f;
+      }
+      acc0 = acc0 + g0[jj] * a0;
+      acc1 = acc1 + g1[jj] * a1;
+    }
+    x0 = nx0;
+    x1 = nx1;
+    h0 = nh0;
+    h1 = nh1;
+    asm volatile("" : "+v"(acc0), "+v"(acc1));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int CMAX>
+__global__ __launch_bounds__(64 * kRsWaves, 1) void resample_rs(RsArgs a) {
+  __shared__ __attribute__((aligned(16))) float ring[kRsLanes * kRsColStride];
+  constexpr int U = (CMAX + 3 + 3) / 4 * 4;                 // shifted row length
+  constexpr int TPT = (kRsPG * U + 64 * kRsWaves - 1) / (64 * kRsWaves);  // tap floats per thread
+  __shared__ __attribute__((aligned(16))) float trow[kRsPG * U];  // this group's rows, pre-shifted
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+  const int ncb = (a.ncols + kRsLanes - 1) / kRsLanes;
+  const int per = (ncb + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int cbA = (int)blockIdx.x * per;
+  const int cbB = cbA + per < ncb ? cbA + per : ncb;
+  if (cbA >= cbB) return;
+  // ring coordinates: rel = pos - t*M - base0, base0 = -(CMAX-1) rounded down to a multiple of 4
+  constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
+  // chunk range [lo, hi) of rel/4 that phase group g needs: its lowest phase's
+  // oldest input .. its highest phase's newest input (phi*M < 2^31 on every path)
+  auto need = [&](int g, int& lo, int& hi) {
+    const int p0 = g * kRsPG;
+    const int p1 = min(p0 + kRsPG, a.up) - 1;
+    const int q0 = p0 * a.down / a.up, q1 = p1 * a.down / a.up;
+    lo = (q0 - (CMAX - 1) - base0) >> 2;
+    hi = ((q1 - base0) >> 2) + 1;
+  };
+  const int lane_ring = ln * kRsColStride;
+  // group g's tap rows: trow[k*U + u] = hs[A(phi)][p(phi)][u], phi = 32g + k
+  auto fetch_taps = [&](int g, float (&tv)[TPT]) {
+#pragma unroll
+    for (int r = 0; r < TPT; ++r) {
+      const int idx = threadIdx.x + r * 64 * kRsWaves;
+      tv[r] = 0.0f;
+      if (idx < kRsPG * U) {
+        const int k = idx / U, u = idx - k * U;
+        const int phi = g * kRsPG + k;
+        if (phi < a.up) {
+          const int q = phi * a.down / a.up;
+          const int A = (q - base0) & 3;
+          const int p = phi * a.down % a.up;
+          tv[r] = a.hs[(A * a.up + p) * a.U + u];
+        }
+      }
+    }
+  };
+  auto store_taps = [&](const float (&tv)[TPT]) {
+#pragma unroll
+    for (int r = 0; r < TPT; ++r) {
+      const int idx = threadIdx.x + r * 64 * kRsWaves;
+      if (idx < kRsPG * U) trow[idx] = tv[r];
+    }
+  };
+  float tv[TPT];
+
+  for (int cb = cbA; cb < cbB; ++cb) {
+    // a new column block: the first group's whole window
+    int lo, hi;
+    need(0, lo, hi);
+    if (a.ablate != 1) {
+      rs_dma<CMAX>(a, ring, cb, wv, ln, base0, lo, hi);
+      rs_edge<CMAX>(a, ring, cb, wv, ln, base0, lo, hi);
+    }
+    fetch_taps(0, tv);
+    store_taps(tv);
+    __syncthreads();
+    int have = hi;  // chunks [.., have) of this block are in the rings
+    for (int g = 0; g < a.ngrp; ++g) {
+      // the next group's new chunks are fetched while this group computes
+      int nlo = 0, nhi = 0;
+      const bool more = g + 1 < a.ngrp;
+      if (more) {
+        need(g + 1, nlo, nhi);
+        nlo = have;
+        if (a.ablate != 1 && nhi > nlo) rs_dma<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
+        fetch_taps(g + 1, tv);  // registers; written to LDS after this group is done
+      }
+      // this wave's two phases
+      const int pa = g * kRsPG + wv, pb = pa + kRsWaves;
+      if (pa < a.up && a.ablate != 2) {
+        const bool on1 = pb < a.up;
+        const int pbb = on1 ? pb : pa;
+        const int qa = pa * a.down / a.up, qb = pbb * a.down / a.up;
+        const int e1a = qa - base0, e1b = qb - base0;  // ring rel of the newest input
+        const int Aa = e1a & 3, Ab = e1b & 3;
+        // the shifted row puts tap i at u = i + 3 - A, input rel e1 - i = 4*(e1 >> 2) + 3 - u:
+        // chunk cc (u = 4cc..4cc+3) is ring chunk (e1 >> 2) - cc
+        const int ctopa = e1a >> 2, ctopb = e1b >> 2;
+        float acc0 = 0.0f, acc1 = 0.0f;
+        rs_scan<CMAX>(acc0, acc1, ring + lane_ring, ctopa, ctopb, Aa, Ab, trow + wv * U,
+                      trow + (on1 ? wv + kRsWaves : wv) * U);
+        const int col = cb * kRsLanes + ln;
+        if (col < a.ncols) {
+          const int s = col / a.np, t = col - s * a.np;
+          const long long ja = (long long)a.up * t + pa, jb = (long long)a.up * t + pb;
+          float* ys = a.y + (long long)s * a.y_stride;
+          if (ja < a.ny) ys[ja] = acc0;
+          if (on1 && jb < a.ny) ys[jb] = acc1;
+        }
+      }
+      if (more && a.ablate != 1 && nhi > nlo) rs_edge<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
+      if (more) have = nhi > have ? nhi : have;
+      __syncthreads();  // the next group's chunks have landed; this group's reads are done
+      if (more) {
+        store_taps(tv);
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// hs[A][p][u] = h[p + (u + A - 3) * L] for 0 <= u + A - 3 < CMAX, else 0.
+__global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h, int ntaps, int up, int cmax,
+                                                     int U, float* hs) {
+  const long long idx = (long long)blockIdx.x * kWG + threadIdx.x;
+  const long long tot = 4LL * up * U;
+  if (idx >= tot) return;
+  const int u = (int)(idx % U);
+  const int p = (int)((idx / U) % up);
+  const int A = (int)(idx / ((long long)U * up));
+  const int i = u + A - 3;
+  const long long k = (long long)p + (long long)i * up;
+  hs[idx] = (i >= 0 && i < cmax && k < ntaps) ? h[k] : 0.0f;
+}
+
+bool rs_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SDR_RESAMPLE_RS");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+}  // namespace
+
+size_t resample_rs_scratch_floats(int up, int ntaps) {
+  const int cmax = (ntaps + up - 1) / up;
+  const int U = (cmax + 3 + 3) / 4 * 4;
+  return (size_t)4 * up * U;
+}
+
+// Returns false (nothing launched) when the shape is not one this kernel
+// covers; the caller then takes the phase-major kernel of resample.hip.
+bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
+                        const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
+                        float* scratch, hipStream_t st, hipError_t* err) {
+  const int cmax = (ntaps + up - 1) / up;
+  if (!rs_enabled() || up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
+  // 16-B chunks straight from the rows
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (nstreams > 1 && x_stride % 4)) return false;
+  // the ring must hold a group's whole window plus the next group's new inputs
+  const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
+  const long long step = ((long long)kRsPG * down + up - 1) / up + 8;
+  if (span + step > kRsRing) return false;
+  const int U = (cmax + 3 + 3) / 4 * 4;
+  const long long tab = 4LL * up * U;
+  hipLaunchKernelGGL(build_shifted, dim3((unsigned)((tab + kWG - 1) / kWG)), dim3(kWG), 0, st, h, ntaps, up, cmax, U,
+                     scratch);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    *err = e;
+    return true;
+  }
+  RsArgs a;
+  a.x = x;
+  a.n = n;
+  a.x_stride = x_stride;
+  a.hs = scratch;
+  a.U = U;
+  a.up = up;
+  a.down = down;
+  a.state = state;
+  a.ns = ns;
+  a.y = y;
+  a.y_stride = y_stride;
+  a.ny = ny;
+  a.np = (int)((ny + up - 1) / up);
+  if ((long long)a.np * nstreams > 0x7fffffffLL - kRsLanes || (long long)up * down > 0x7fffffffLL) return false;
+  a.ncols = a.np * nstreams;
+  a.ngrp = (up + kRsPG - 1) / kRsPG;
+  static const int ablate = [] {
+    const char* v = std::getenv("SDR_ABLATE");
+    return v ? std::atoi(v) : 0;
+  }();
+  a.ablate = ablate;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int ncb = (a.ncols + kRsLanes - 1) / kRsLanes;
+  const int grid = ncb < ncu ? ncb : ncu;
+  if (cmax == 151)
+    hipLaunchKernelGGL(resample_rs<151>, dim3((unsigned)grid), dim3(64 * kRsWaves), 0, st, a);
+  else
+    hipLaunchKernelGGL(resample_rs<101>, dim3((unsigned)grid), dim3(64 * kRsWaves), 0, st, a);
+  *err = hipGetLastError();
+  return true;
+}
+
+}  // namespace sdr

@@ -95,5 +95,10 @@ bool fir_has_fast_path(int D, int ntaps, int ns, int nch, bool demod, Src src);
 
 // Bytes of scratch the resampler needs for its polyphase tap table.
 size_t resample_scratch_floats(int up, int ntaps);
+// Sliding-window resampler (resample_rs.hip): false = shape not covered.
+size_t resample_rs_scratch_floats(int up, int ntaps);
+bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
+                        const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
+                        float* scratch, hipStream_t st, hipError_t* err);
 
 }  // namespace sdr
