@@ -313,12 +313,10 @@ __global__ __launch_bounds__(kWG) void resample_commit(const float* __restrict__
   state[(long long)s * ns + i] = x[(long long)s * x_stride + n - ns + i];
 }
 
+// read per launch (a getenv scan), so a test can switch kernels in-process
 bool pp_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("SDR_RESAMPLE_PP");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
+  const char* e = std::getenv("SDR_RESAMPLE_PP");
+  return !e || std::atoi(e) != 0;
 }
 
 }  // namespace

@@ -36,6 +36,11 @@ constexpr int kRsRingC = kRsRing / 4;
 // (same ring offset, different columns) start on different banks
 constexpr int kRsColStride = kRsRing + 4;
 
+// LDS-DMA writes are counted by vmcnt, which the workgroup fence of
+// __syncthreads() does not wait for: every wave drains its own DMAs before a
+// barrier that publishes them to the other waves.
+__device__ __forceinline__ void dma_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 struct RsArgs {
   const float* x;
   long long n, x_stride;
@@ -219,6 +224,7 @@ __global__ __launch_bounds__(64 * kRsWaves, 1) void resample_rs(RsArgs a) {
     }
     fetch_taps(0, tv);
     store_taps(tv);
+    dma_drain();
     __syncthreads();
     int have = hi;  // chunks [.., have) of this block are in the rings
     for (int g = 0; g < a.ngrp; ++g) {
@@ -256,6 +262,7 @@ __global__ __launch_bounds__(64 * kRsWaves, 1) void resample_rs(RsArgs a) {
       }
       if (more && a.ablate != 1 && nhi > nlo) rs_edge<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
       if (more) have = nhi > have ? nhi : have;
+      dma_drain();
       __syncthreads();  // the next group's chunks have landed; this group's reads are done
       if (more) {
         store_taps(tv);
@@ -279,12 +286,258 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
   hs[idx] = (i >= 0 && i < cmax && k < ntaps) ? h[k] : 0.0f;
 }
 
+// ---------------------------------------------------------------------------
+// resample_lp: lane = (phase, column subset), taps in VGPRs.
+//
+// Workgroup = 7 waves = 448 lanes; lane slots hold (phi, sub) items, phi < L,
+// sub < S = floor(448 / L) (S = 3 at L = 147).  A lane keeps its phase's
+// shifted tap row (U floats) in VGPRs for the whole launch and computes the
+// outputs of that phase for columns c = sub + S*k, k < K (K accumulation
+// chains), reading its inputs from an LDS image of the item's span with
+// 16-B ds_read_b128 (aligned because the row is pre-shifted by the lane's
+// A).  Per multiply-add only 4 B of LDS are read (no tap traffic), which is
+// half of what the column-lane kernels above read.  Work item = (stream,
+// batch of up to S*K consecutive columns); the next item's span is brought
+// in by LDS-DMA into the other buffer while the current one is computed.
+//
+// Lane placement: ds_read_b128 serves a wave in four groups of 16 lanes, and
+// two lanes of one group conflict when their chunk indices differ by a
+// multiple of 16 (64 banks).  A lane's chunk index mod 16 is fixed for the
+// launch ((sub*M/4 + ctop(phi)) mod 16, the column stride adds the same
+// amount to every lane), so build_lanes() sorts the items by that class and
+// deals them round-robin over the 28 groups: a group gets two items of one
+// class only when the class has more than 28 items.
+constexpr int kLpWaves = 7;
+constexpr int kLpSlots = 64 * kLpWaves;
+constexpr int kLpGroups = kLpSlots / 16;
+constexpr int kLpBuf = 19456;  // floats per staging buffer (76 KiB); two buffers
+
+struct LpArgs {
+  const float* x;
+  long long n, x_stride;
+  const float* hs;   // [4][L][U] shifted taps (build_shifted)
+  const int* lanes;  // [kLpSlots]: phi | sub << 16, or -1
+  int up, down;
+  const float* state;
+  int ns;
+  float* y;
+  long long y_stride, ny;
+  int np;      // columns (periods) per stream
+  int C;       // columns per item
+  int nbat;    // items per stream
+  int nitems;  // nstreams * nbat
+  int S;       // column subsets
+  int ablate;
+};
+
+// lanes of each ds_read_b128 lane group (MI355X_MICROARCH.md, LDS table)
+__constant__ unsigned char kB128Groups[4][16] = {
+    {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+    {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+    {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+    {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+
+// One workgroup: counting sort of the L*S items by bank class, then deal.
+__global__ __launch_bounds__(kLpSlots) void build_lanes(int up, int down, int S, int base0, int* lanes) {
+  __shared__ int cnt[16], start[16], fill[16];
+  __shared__ int order[kLpSlots];
+  const int t = threadIdx.x;
+  const int nit = up * S;
+  if (t < 16) {
+    cnt[t] = 0;
+    fill[t] = 0;
+  }
+  lanes[t] = -1;
+  __syncthreads();
+  int cls = -1;
+  if (t < nit) {
+    const int phi = t % up, sub = t / up;
+    const int q = (int)((long long)phi * down / up);
+    cls = ((sub * (down / 4)) + ((q - base0) >> 2)) & 15;
+    atomicAdd(&cnt[cls], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int c = 0; c < 16; ++c) {
+      start[c] = acc;
+      acc += cnt[c];
+    }
+  }
+  __syncthreads();
+  if (t < nit) order[start[cls] + atomicAdd(&fill[cls], 1)] = t;
+  __syncthreads();
+  if (t < nit) {
+    // position r in class order -> group r mod 28, member r / 28
+    const int g = t % kLpGroups, m = t / kLpGroups;
+    const int item = order[t];
+    const int lane = (g >> 2) * 64 + kB128Groups[g & 3][m];
+    lanes[lane] = (item % up) | ((item / up) << 16);
+  }
+}
+
+// Stage item `it` (its whole input span) into buf: LDS-DMA for the chunks
+// inside [0, n), registers for the chunks that reach into the carried state
+// or past the end.
+template <int CMAX>
+__device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, int wv, int ln) {
+  constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
+  const int st = it / a.nbat, b = it - st * a.nbat;
+  const int t0 = b * a.C;
+  const int ce = min(a.C, a.np - t0);
+  const long long P0 = (long long)t0 * a.down + base0;
+  const int qmax = (int)((long long)(a.up - 1) * a.down / a.up);
+  const int W = (ce - 1) * a.down + qmax + 1 - base0;
+  const int nch = (W + 3) >> 2;
+  const float* xs = a.x + (long long)st * a.x_stride;
+  // DMA: chunk j covers positions P0 + 4j .. +3; lanes of one instruction are consecutive chunks
+  const long long jlo = P0 < 0 ? (-P0 + 3) >> 2 : 0;          // first chunk with g >= 0
+  long long jhi = (a.n - P0) >> 2;                             // chunks j < jhi end inside [0, n)
+  if (jhi > nch) jhi = nch;
+  // edges first (chunks below jlo and from jhi up): their register loads then
+  // do not wait behind this item's DMAs
+  const int tid = threadIdx.x;
+  auto edge = [&](int j) {
+    const long long g = P0 + 4LL * j;
+    float w4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long gg = g + r;
+      w4[r] = gg >= 0 ? (gg < a.n ? xs[gg] : 0.0f) : (gg >= -a.ns ? a.state[(long long)st * a.ns + a.ns + gg] : 0.0f);
+    }
+    *reinterpret_cast<float4*>(buf + 4 * j) = make_float4(w4[0], w4[1], w4[2], w4[3]);
+  };
+  for (int j = tid; j < (int)jlo && j < nch; j += kLpSlots) edge(j);
+  for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += kLpSlots) edge(j);
+  // DMA: lanes of one instruction are consecutive chunks
+  for (int j0 = (int)(jlo & ~63LL) + wv * 64; j0 < jhi; j0 += 64 * kLpWaves) {
+    const int j = j0 + ln;
+    if (j >= jlo && j < jhi) __builtin_amdgcn_global_load_lds(xs + P0 + 4LL * j, buf + 4 * j0, 16, 0, 0);
+  }
+}
+
+template <int CMAX, int K>
+__device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, int it, const float (&tp)[(CMAX + 6) / 4 * 4],
+                                           int phi, int sub, int A, int ctop0, bool valid) {
+  constexpr int NC = (CMAX + 6) / 4;
+  const int st = it / a.nbat, b = it - st * a.nbat;
+  const int t0 = b * a.C;
+  const int ce = min(a.C, a.np - t0);
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const f4v lds4;
+  lds4* ptr[K];  // chunk (ctop - (NC-1)) of each chain; chunk ctop - cc sits at ptr + (NC-1-cc)
+  bool act[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = sub + a.S * k;
+    act[k] = valid && c < ce;
+    const int cc = c < ce ? c : 0;
+    ptr[k] = (lds4*)(buf + 4 * (cc * (a.down >> 2) + ctop0 - (NC - 1)));
+    asm volatile("" : "+v"(ptr[k]));  // keep the base in a VGPR: per-chunk offsets stay immediates
+  }
+  float acc[K];
+  f4v cur[K], nxt[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    acc[k] = 0.0f;
+    cur[k] = ptr[k][NC - 1];
+  }
+#pragma unroll
+  for (int cc = 0; cc < NC; ++cc) {
+    // the next chunk's reads go out first; this chunk's were issued one chunk ago
+    if (cc + 1 < NC) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) nxt[k] = ptr[k][NC - 2 - cc];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int jj = 3; jj >= 0; --jj) {
+      const int u = 4 * cc + 3 - jj;
+      // i = u + A - 3 must lie in [0, CMAX) -- only at the two ends; there the
+      // shifted tap is 0 and the input is replaced by 0 (term +0: acc unchanged)
+      const bool edge = (cc == 0) || (u >= CMAX);
+      const bool ok = !edge || (u + A - 3 >= 0 && u + A - 3 < CMAX);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float v = cur[k][jj];
+        if (edge) v = ok ? v : 0.0f;
+        acc[k] = acc[k] + tp[u] * v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cur[k] = nxt[k];
+      asm volatile("" : "+v"(acc[k]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float* ys = a.y + (long long)st * a.y_stride;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long long j = (long long)a.up * (t0 + sub + a.S * k) + phi;
+    if (act[k] && j < a.ny) ys[j] = acc[k];
+  }
+}
+
+template <int CMAX, int K>
+__global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
+  __shared__ __attribute__((aligned(16))) float bufA[kLpBuf];
+  __shared__ __attribute__((aligned(16))) float bufB[kLpBuf];
+  constexpr int U = (CMAX + 6) / 4 * 4;
+  constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+  // this lane's item and taps, for the whole launch
+  const int code = a.lanes[threadIdx.x];
+  const bool valid = code >= 0;
+  const int phi = valid ? (code & 0xffff) : 0, sub = valid ? (code >> 16) : 0;
+  const int q = (int)((long long)phi * a.down / a.up);
+  const int A = (q - base0) & 3, ctop0 = (q - base0) >> 2;
+  const int p = (int)((long long)phi * a.down % a.up);
+  float tp[U];
+  const float* row = a.hs + ((long long)A * a.up + p) * U;
+#pragma unroll
+  for (int u = 0; u < U; u += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(row + u);
+    tp[u] = v.x;
+    tp[u + 1] = v.y;
+    tp[u + 2] = v.z;
+    tp[u + 3] = v.w;
+  }
+  // items: contiguous range per workgroup
+  const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
+  if (i0 >= i1) return;
+  if (a.ablate != 1) lp_stage<CMAX>(a, bufA, i0, wv, ln);
+  for (int it = i0; it < i1; ++it) {
+    dma_drain();
+    __syncthreads();  // item it's span has landed; the other buffer is free
+    const bool odd = ((it - i0) & 1) != 0;
+    if (it + 1 < i1 && a.ablate != 1) {
+      if (odd)
+        lp_stage<CMAX>(a, bufA, it + 1, wv, ln);
+      else
+        lp_stage<CMAX>(a, bufB, it + 1, wv, ln);
+    }
+    if (a.ablate != 2) {
+      if (odd)
+        lp_compute<CMAX, K>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
+      else
+        lp_compute<CMAX, K>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
+    }
+  }
+}
+
+// read per launch (a getenv scan), so a test can switch kernels in-process
+bool lp_enabled() {
+  const char* e = std::getenv("SDR_RESAMPLE_LP");
+  return !e || std::atoi(e) != 0;
+}
+
+// read per launch (a getenv scan), so a test can switch kernels in-process
 bool rs_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("SDR_RESAMPLE_RS");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
+  const char* e = std::getenv("SDR_RESAMPLE_RS");
+  return !e || std::atoi(e) != 0;
 }
 
 }  // namespace
@@ -292,7 +545,7 @@ bool rs_enabled() {
 size_t resample_rs_scratch_floats(int up, int ntaps) {
   const int cmax = (ntaps + up - 1) / up;
   const int U = (cmax + 3 + 3) / 4 * 4;
-  return (size_t)4 * up * U;
+  return (size_t)4 * up * U + kLpSlots;  // shifted rows + the lane table of resample_lp
 }
 
 // Returns false (nothing launched) when the shape is not one this kernel
@@ -301,13 +554,18 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
                         float* scratch, hipStream_t st, hipError_t* err) {
   const int cmax = (ntaps + up - 1) / up;
-  if (!rs_enabled() || up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
+  if (up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
   // 16-B chunks straight from the rows
   if ((reinterpret_cast<uintptr_t>(x) & 15) || (nstreams > 1 && x_stride % 4)) return false;
-  // the ring must hold a group's whole window plus the next group's new inputs
+  // resample_lp: the staging buffer must hold at least one column's span
+  const int base0 = -(((cmax - 1) + 3) / 4 * 4);
+  const int qmax = (int)((long long)(up - 1) * down / up);
+  const bool use_lp = lp_enabled() && up <= kLpSlots && (long long)up * down < (1LL << 31) &&
+                      qmax + 1 - base0 + 4 <= kLpBuf;
+  // resample_rs: the ring must hold a group's whole window plus the next group's new inputs
   const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
   const long long step = ((long long)kRsPG * down + up - 1) / up + 8;
-  if (span + step > kRsRing) return false;
+  if (!use_lp && (!rs_enabled() || span + step > kRsRing)) return false;
   const int U = (cmax + 3 + 3) / 4 * 4;
   const long long tab = 4LL * up * U;
   hipLaunchKernelGGL(build_shifted, dim3((unsigned)((tab + kWG - 1) / kWG)), dim3(kWG), 0, st, h, ntaps, up, cmax, U,
@@ -316,6 +574,63 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   if (e != hipSuccess) {
     *err = e;
     return true;
+  }
+  static const int ablate = [] {
+    const char* v = std::getenv("SDR_ABLATE");
+    return v ? std::atoi(v) : 0;
+  }();
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int np = (int)((ny + up - 1) / up);
+  if (use_lp) {
+    // columns per item: S*K chains, bounded by the staging buffer
+    const int S = kLpSlots / up;
+    const int K = (np <= 4 * S) ? 4 : 7;
+    int C = S * K;
+    const long long fit = (kLpBuf - (qmax + 1 - base0) - 4) / down + 1;
+    if (C > fit) C = (int)fit;
+    if (C > np) C = np;
+    if (C < 1) C = 1;
+    {
+      LpArgs b;
+      b.x = x;
+      b.n = n;
+      b.x_stride = x_stride;
+      b.hs = scratch;
+      b.lanes = reinterpret_cast<int*>(scratch + tab);
+      b.up = up;
+      b.down = down;
+      b.state = state;
+      b.ns = ns;
+      b.y = y;
+      b.y_stride = y_stride;
+      b.ny = ny;
+      b.np = np;
+      b.C = C;
+      b.nbat = (np + C - 1) / C;
+      b.nitems = b.nbat * nstreams;
+      b.S = S;
+      b.ablate = ablate;
+      hipLaunchKernelGGL(build_lanes, dim3(1), dim3(kLpSlots), 0, st, up, down, S, base0, const_cast<int*>(b.lanes));
+      const int grid = b.nitems < ncu ? b.nitems : ncu;
+      if (cmax == 151) {
+        if (K == 4)
+          hipLaunchKernelGGL((resample_lp<151, 4>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
+        else
+          hipLaunchKernelGGL((resample_lp<151, 7>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
+      } else {
+        if (K == 4)
+          hipLaunchKernelGGL((resample_lp<101, 4>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
+        else
+          hipLaunchKernelGGL((resample_lp<101, 7>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
+      }
+      *err = hipGetLastError();
+      return true;
+    }
   }
   RsArgs a;
   a.x = x;
@@ -330,21 +645,11 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   a.y = y;
   a.y_stride = y_stride;
   a.ny = ny;
-  a.np = (int)((ny + up - 1) / up);
+  a.np = np;
   if ((long long)a.np * nstreams > 0x7fffffffLL - kRsLanes || (long long)up * down > 0x7fffffffLL) return false;
   a.ncols = a.np * nstreams;
   a.ngrp = (up + kRsPG - 1) / kRsPG;
-  static const int ablate = [] {
-    const char* v = std::getenv("SDR_ABLATE");
-    return v ? std::atoi(v) : 0;
-  }();
   a.ablate = ablate;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
   const int ncb = (a.ncols + kRsLanes - 1) / kRsLanes;
   const int grid = ncb < ncu ? ncb : ncu;
   if (cmax == 151)

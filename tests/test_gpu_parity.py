@@ -149,13 +149,26 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
         assert_bits(s_g, s_o, "state")
 
 
-@pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560),
-                                               (3, 7, 101, 100, 700), (5, 2, 151, 150, 400),
-                                               (147, 800, 151, 150, 65600)])
-def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, n):
-    """Phase-major tiled resampler (T = cnt*up): several streams per launch
-    (64-column blocks cross stream boundaries), 16-B and dword staging
-    (down % 4), up < 16 phase groups, multi-block state carry."""
+RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
+                  (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
+                  (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
+# resample_lp (default), then resample_rs, then the phase-major resample_pp
+RESAMPLE_KERNELS = {"lp": {}, "rs": {"SDR_RESAMPLE_LP": "0"},
+                    "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
+
+
+@pytest.mark.parametrize("kernel", list(RESAMPLE_KERNELS))
+@pytest.mark.parametrize("up,down,cnt,ns,n", RESAMPLE_CASES)
+def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
+    """Batched resampler (T = cnt*up) on each of its kernels -- lane-phase
+    (taps in VGPRs), sliding-window and phase-major: several streams per
+    launch, 16-B and dword staging (down % 4), small and large up (column
+    subsets), items that start inside the carried state, ragged last
+    batches, multi-block state carry.  The kernel is chosen per launch from
+    SDR_RESAMPLE_{LP,RS,PP}; shapes a kernel does not cover fall through to
+    the next one, so every case is checked under every setting."""
+    for k, v in RESAMPLE_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
     sdrhip = built_lib
     nstreams = 5 if n < 10000 else 2
     rng = np.random.default_rng(up * 1000 + down)
