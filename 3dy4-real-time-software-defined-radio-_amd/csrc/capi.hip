@@ -18,14 +18,14 @@ struct sdr_ctx {
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
   // grow-only device scratch for the host-pointer wrappers and internal use
-  void* buf[13] = {};
-  size_t cap[13] = {};
+  void* buf[17] = {};
+  size_t cap[17] = {};
   std::string err;
 };
 
 namespace {
 
-enum Slot { kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp, kPipe0, kPipe1, kPipe2 };
+enum Slot { kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp, kPipe0, kPipe1, kPipe2, kPipe3, kPipe4, kPipe5, kPipe6 };
 
 int fail(sdr_ctx* c, int code, const char* fmt, ...) {
   if (c) {
@@ -473,6 +473,83 @@ int sdr_mono_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
                                  ns_audio, audio, astride)))
     return rc;
   return sdr_pcm_s16_dev(c, audio, na, nstreams, astride, pcm, pcm_stride);
+}
+
+int sdr_fm_pll_dev(sdr_ctx* c, const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
+                   float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
+                   long long mix_stride, float* out, long long out_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!in || !pll || !out) return fail(c, SDR_EINVAL, "null pointer");
+  if (n <= 0 || nstreams < 1) return fail(c, SDR_EINVAL, "empty block (fmPLL writes ncoOut[0], filter.cpp:186)");
+  if (nstreams > 1 && (in_stride < n || out_stride < n || (mix && mix_stride < n)))
+    return fail(c, SDR_EINVAL, "stream strides overlap");
+  hipError_t e = sdr::launch_pll(in, n, nstreams, in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix,
+                                 mix_stride, out, out_stride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "pll launch");
+  return SDR_OK;
+}
+
+int sdr_stereo_pcm_dev(sdr_ctx* c, const float* mono, const float* stereo, long long n, int nstreams,
+                       long long stride, int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!mono || !stereo || !pcm || n < 0 || nstreams < 1) return fail(c, SDR_EINVAL, "bad stereo pcm arguments");
+  if (nstreams > 1 && (stride < n || pcm_stride < 2 * n)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  if (n == 0) return SDR_OK;
+  hipError_t e = sdr::launch_stereo_pcm(mono, stereo, n, nstreams, stride, pcm, pcm_stride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "stereo pcm launch");
+  return SDR_OK;
+}
+
+int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
+                          int up, int down, float audio_fs, const sdr_stereo_taps* taps, sdr_stereo_state* st,
+                          int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!taps || !st) return fail(c, SDR_EINVAL, "null taps / state");
+  if (D < 1 || npairs <= 0 || npairs % D) return fail(c, SDR_EINVAL, "block of %lld pairs is not a multiple of %d",
+                                                   npairs, D);
+  const long long nd = npairs / D;
+  const long long na = sdr_resample_out_len(up, down, nd);
+  if (na <= 0) return fail(c, SDR_EINVAL, "empty audio block");
+  if (nstreams > 1 && pcm_stride < 2 * na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
+  const long long dstride = (nd + 3) / 4 * 4, astride = (na + 3) / 4 * 4;
+  const size_t dbytes = (size_t)nstreams * dstride * sizeof(float), abytes = (size_t)nstreams * astride * sizeof(float);
+  float* demod = static_cast<float*>(scratch(c, kPipe0, dbytes));
+  float* work = static_cast<float*>(scratch(c, kPipe1, dbytes));  // delayed demod, then the mixer output
+  float* mono = static_cast<float*>(scratch(c, kPipe2, abytes));
+  float* pilot = static_cast<float*>(scratch(c, kPipe3, dbytes));
+  float* sband = static_cast<float*>(scratch(c, kPipe4, dbytes));
+  float* slp = static_cast<float*>(scratch(c, kPipe5, abytes));
+  if (!demod || !work || !mono || !pilot || !sband || !slp) return fail(c, SDR_ENOMEM, "pipeline buffers");
+  // src/project.cpp:72-93: front end
+  if ((rc = sdr_frontend_u8_dev(c, D, iq, npairs, nstreams, iq_stride, taps->h_rf, taps->rf_taps, st->state_i,
+                                st->state_q, st->ns_rf, st->prev_i, st->prev_q, demod, dstride)))
+    return rc;
+  // :114-116: mono = resample(delay(demod))
+  if ((rc = sdr_delay_f32_dev(c, demod, nd, nstreams, dstride, st->delay_state, st->ns_delay, work, dstride)))
+    return rc;
+  if ((rc = sdr_resample_f32_dev(c, up, down, work, nd, nstreams, dstride, taps->h_audio, taps->audio_taps,
+                                 st->state_audio, st->ns_audio, mono, astride)))
+    return rc;
+  // :120-121: pilot and stereo band-pass filters on the undelayed demod
+  if ((rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_pilot, taps->bpf_taps, st->pilot_state,
+                                  st->ns_bpf, pilot, dstride)))
+    return rc;
+  if ((rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_stereo, taps->bpf_taps,
+                                  st->stereo_state, st->ns_bpf, sband, dstride)))
+    return rc;
+  // :123-126: PLL on the pilot (19 kHz, ncoScale 2, phaseAdjust 0, bandwidth 0.01) fused with the mixer
+  if ((rc = sdr_fm_pll_dev(c, pilot, nd, nstreams, dstride, 19e3f, audio_fs, 2.0f, 0.0f, 0.01f, st->pll, sband,
+                           dstride, work, dstride)))
+    return rc;
+  // :129: the stereo channel through the same audio resampler, its own state
+  if ((rc = sdr_resample_f32_dev(c, up, down, work, nd, nstreams, dstride, taps->h_audio, taps->audio_taps,
+                                 st->stereo_lp_state, st->ns_audio, slp, astride)))
+    return rc;
+  // :131-132 + 304-314: L/R, interleave, s16
+  return sdr_stereo_pcm_dev(c, mono, slp, na, nstreams, astride, pcm, pcm_stride);
 }
 
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

@@ -25,22 +25,13 @@ __global__ __launch_bounds__(kWG) void delay_kernel(const float* __restrict__ in
   }
 }
 
-// src/project.cpp:311-314: NaN -> 0, else static_cast<short>(x * 16384) as
-// the reference's compiler emits it (truncate to int32, keep the low 16
-// bits; values outside int32 give INT_MIN -> 0).
+// src/project.cpp:311-314 (pcm_quantise, sdr_common.hpp)
 __global__ __launch_bounds__(kWG) void pcm_kernel(const float* __restrict__ x, long long n, long long x_stride,
                                                   int16_t* __restrict__ pcm, long long pcm_stride) {
   const int s = blockIdx.y;
   const long long i = (long long)blockIdx.x * kWG + threadIdx.x;
   if (i >= n) return;
-  const float u = x[(long long)s * x_stride + i];
-  int16_t r = 0;
-  if (!__builtin_isnan(u)) {
-    const float v = u * 16384.0f;
-    const int w = (v < 2147483648.0f && v >= -2147483648.0f) ? (int)v : (int)0x80000000u;
-    r = (int16_t)(uint16_t)((unsigned)w & 0xffffu);
-  }
-  pcm[(long long)s * pcm_stride + i] = r;
+  pcm[(long long)s * pcm_stride + i] = pcm_quantise(x[(long long)s * x_stride + i]);
 }
 
 }  // namespace

@@ -72,10 +72,27 @@ hipError_t launch_delay(const float* in, long long n, int nstreams, long long in
                         float* out, long long out_stride, hipStream_t st);
 hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
                       long long pcm_stride, hipStream_t st);
+// Stereo back end (stereo.hip): fmPLL one lane per stream, optionally fused
+// with the x2 mixer; L/R + interleave + s16 output stage.
+hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
+                      float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
+                      long long mix_stride, float* out, long long out_stride, hipStream_t st);
+hipError_t launch_stereo_pcm(const float* a, const float* b, long long n, int nstreams, long long stride,
+                             int16_t* pcm, long long pcm_stride, hipStream_t st);
 hipError_t launch_synth_fm_u8(uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
                               unsigned long long seed, hipStream_t st);
 hipError_t launch_u8_to_planar(const uint8_t* iq, long long npairs, int nstreams, long long iq_stride, float* I,
                                float* Q, long long x_stride, hipStream_t st);
+
+// src/project.cpp:311-314: NaN -> 0, else static_cast<short>(x * 16384) as
+// the reference's x86-64 build emits it (cvttss2si to int32, keep the low 16
+// bits; values outside int32 give INT_MIN -> 0).
+__device__ __forceinline__ int16_t pcm_quantise(float u) {
+  if (__builtin_isnan(u)) return 0;
+  const float v = u * 16384.0f;
+  const int w = (v < 2147483648.0f && v >= -2147483648.0f) ? (int)v : (int)0x80000000u;
+  return (int16_t)(uint16_t)((unsigned)w & 0xffffu);
+}
 
 // Long FIRs without decimation (fir_long.hip): T a multiple of 32.
 bool fir_long_ok(int D, int ntaps, int ns, long long n);

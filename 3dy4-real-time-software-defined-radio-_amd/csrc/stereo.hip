@@ -1,0 +1,97 @@
+// stereo.hip -- the device-resident stereo back end around the front end
+// (stereo half): the pilot PLL
+// (src/filter.cpp:174-228) fused with the stereo mixer (pointwiseMultiply,
+// :253-266), and the output stage that forms L = mono + stereo,
+// R = mono - stereo (:267-288), interleaves them (:289-301) and quantises to
+// s16 (src/project.cpp:307-314).  The band-pass filters and both resamplers
+// are the FIR / resampler kernels of fir_tile.hip / resample*.hip.
+//
+// fmPLL is a sequential recurrence (each sample's phase detector reads the
+// previous sample's NCO), so it runs one lane per stream: streams are the
+// parallel axis, samples are a loop.  Arithmetic follows the reference's
+// promotions exactly: the loop filter in fp32, atan2 / cos / sin of the fp32
+// arguments in double (the reference calls the double C functions), every
+// result rounded back to float where the reference stores a float.
+#include "sdr_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace sdr {
+namespace {
+
+constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
+
+// pll[6] per stream: feedbackI, feedbackQ, integrator, phaseEst, trigOffset, nco_state
+// (src/project.cpp:48-55).  mix == nullptr: out = ncoOut; else out = ncoOut * mix * 2.
+__global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, long long n, int nstreams,
+                                                 long long in_stride, float freq, float Fs, float nco_scale,
+                                                 float phase_adjust, float norm_bw, float* __restrict__ pll,
+                                                 const float* __restrict__ mix, long long mix_stride,
+                                                 float* __restrict__ out, long long out_stride) {
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= nstreams) return;
+  const float* x = in + (long long)s * in_stride;
+  const float* m = mix ? mix + (long long)s * mix_stride : nullptr;
+  float* y = out + (long long)s * out_stride;
+  float* st = pll + 6LL * s;
+  float fbI = st[0], fbQ = st[1], integrator = st[2], phaseEst = st[3], trigOffset = st[4], nco_prev = st[5];
+  // src/filter.cpp:175-179: float Cp = 2.666, Ci = 3.555; Kp, Ki in float
+  const float Kp = norm_bw * 2.666f;
+  const float Ki = norm_bw * norm_bw * 3.555f;
+  const double step = 2.0 * kPiD * (double)(freq / Fs);  // 2*PI*(freq/Fs), double (PI is a double literal)
+  for (long long k = 0; k < n; ++k) {
+    const float v = x[k];
+    const float eI = (v == 0.0f ? 1.0f : v) * fbI;
+    const float eQ = v * (-1.0f * fbQ);
+    const float eD = (float)atan2((double)eQ, (double)eI);
+    integrator = integrator + Ki * eD;
+    phaseEst = phaseEst + (Kp * eD + integrator);
+    trigOffset = trigOffset + 1.0f;
+    const float arg = (float)(step * (double)trigOffset + (double)phaseEst);
+    fbI = (float)cos((double)arg);
+    fbQ = (float)sin((double)arg);
+    const float nco = (float)cos((double)(arg * nco_scale + phase_adjust));
+    // ncoOut[k] is the previous sample's NCO (ncoOut[0] = nco_state, :186)
+    y[k] = m ? nco_prev * m[k] * 2.0f : nco_prev;
+    nco_prev = nco;
+  }
+  st[0] = fbI;
+  st[1] = fbQ;
+  st[2] = integrator;
+  st[3] = phaseEst;
+  st[4] = trigOffset;
+  st[5] = nco_prev;  // nco_state = the last sample's NCO (:221-222)
+}
+
+// L/R + interleave + s16: pcm[2i] = q(a[i] + b[i]), pcm[2i+1] = q(a[i] - b[i])
+__global__ __launch_bounds__(kWG) void stereo_pcm_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         long long n, long long stride, int16_t* __restrict__ pcm,
+                                                         long long pcm_stride) {
+  const int s = blockIdx.y;
+  const long long i = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (i >= n) return;
+  const float u = a[(long long)s * stride + i], v = b[(long long)s * stride + i];
+  const float l = u + v, r = u - v;
+  int16_t* p = pcm + (long long)s * pcm_stride + 2 * i;
+  p[0] = pcm_quantise(l);
+  p[1] = pcm_quantise(r);
+}
+
+}  // namespace
+
+hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
+                      float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
+                      long long mix_stride, float* out, long long out_stride, hipStream_t st) {
+  hipLaunchKernelGGL(pll_kernel, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams, in_stride,
+                     freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix, mix_stride, out, out_stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_stereo_pcm(const float* a, const float* b, long long n, int nstreams, long long stride,
+                             int16_t* pcm, long long pcm_stride, hipStream_t st) {
+  hipLaunchKernelGGL(stereo_pcm_kernel, dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0, st,
+                     a, b, n, stride, pcm, pcm_stride);
+  return hipGetLastError();
+}
+
+}  // namespace sdr

@@ -78,6 +78,10 @@ _SIGS = {
     "sdr_pcm_s16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _ll],
     "sdr_mono_pcm_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _i,
                             _vp, _i, _vp, _ll],
+    "sdr_fm_pll_dev": [_vp, _vp, _ll, _i, _ll, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _vp, _vp,
+                       _ll, _vp, _ll],
+    "sdr_stereo_pcm_dev": [_vp, _vp, _vp, _ll, _i, _ll, _vp, _ll],
+    "sdr_stereo_pcm_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _i, _i, C.c_float, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
 }
@@ -85,6 +89,19 @@ _RESTYPE = {"sdr_version": C.c_char_p, "sdr_strerror": C.c_char_p, "sdr_ctx_last
             "sdr_ctx_get_stream": _vp, "sdr_resample_out_len": _ll}
 
 EXPORTED = tuple(_SIGS)
+
+
+class StereoTaps(C.Structure):
+    """include/sdr_hip.h sdr_stereo_taps (device pointers)."""
+    _fields_ = [("h_rf", _vp), ("rf_taps", _i), ("h_audio", _vp), ("audio_taps", _i), ("h_pilot", _vp),
+                ("h_stereo", _vp), ("bpf_taps", _i)]
+
+
+class StereoState(C.Structure):
+    """include/sdr_hip.h sdr_stereo_state (device pointers, one row per stream)."""
+    _fields_ = [("state_i", _vp), ("state_q", _vp), ("ns_rf", _i), ("prev_i", _vp), ("prev_q", _vp),
+                ("delay_state", _vp), ("ns_delay", _i), ("state_audio", _vp), ("stereo_lp_state", _vp),
+                ("ns_audio", _i), ("pilot_state", _vp), ("stereo_state", _vp), ("ns_bpf", _i), ("pll", _vp)]
 
 
 class SdrError(RuntimeError):
@@ -315,6 +332,24 @@ class Context:
                                               _ptr(st_i), _ptr(st_q), ns_rf, _ptr(prev_i), _ptr(prev_q),
                                               _ptr(delay_state), ns_delay, up, down, _ptr(h_audio), audio_taps,
                                               _ptr(st_audio), ns_audio, _ptr(pcm), pcm_stride), "mono_pcm_u8_dev")
+
+    def fm_pll_dev(self, x, n, nstreams, x_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix, mix_stride,
+                   out, out_stride):
+        """fmPLL, one lane per stream; mix given: fused with the x2 stereo mixer."""
+        self._check(lib().sdr_fm_pll_dev(self._c, _ptr(x), n, nstreams, x_stride, freq, Fs, nco_scale, phase_adjust,
+                                         norm_bw, _ptr(pll), _ptr(mix), mix_stride, _ptr(out), out_stride),
+                    "fm_pll_dev")
+
+    def stereo_pcm_dev(self, mono, stereo, n, nstreams, stride, pcm, pcm_stride):
+        self._check(lib().sdr_stereo_pcm_dev(self._c, _ptr(mono), _ptr(stereo), n, nstreams, stride, _ptr(pcm),
+                                             pcm_stride), "stereo_pcm_dev")
+
+    def stereo_pcm_u8_dev(self, D, iq, npairs, nstreams, iq_stride, up, down, audio_fs, taps, state, pcm,
+                          pcm_stride):
+        """src/project.cpp's stereo path for one block of every stream: u8 IQ -> interleaved s16 L/R."""
+        self._check(lib().sdr_stereo_pcm_u8_dev(self._c, D, _ptr(iq), npairs, nstreams, iq_stride, up, down,
+                                                audio_fs, C.addressof(taps), C.addressof(state), _ptr(pcm),
+                                                pcm_stride), "stereo_pcm_u8_dev")
 
     def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
         self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")

@@ -54,6 +54,9 @@ CONFIGS = {
     # u8 IQ -> front end -> delay -> audio FIR+dec5 -> s16 PCM, 51,200-pair reference blocks
     "mono0": dict(kind="mono_u8", D=10, up=1, down=5, ntaps=101, n=51200, streams=1024,
                   workload="mode0_mono_u8iq_to_s16pcm_block51200"),
+    # SURVEY 8(f) 2 (stereo half): the whole mode-0 stereo path, PLL one lane per stream
+    "stereo0": dict(kind="stereo_u8", D=10, up=1, down=5, ntaps=101, n=51200, streams=1024,
+                    workload="mode0_stereo_u8iq_to_s16pcm_LR_block51200"),
     # BASELINE config 5's fp16 arm: fp16 storage, fp32 accumulation (v_dot2_f32_f16); not
     # bit-exact -- the line carries its error against the exact fp32 path
     "cfg5h": dict(kind="fir_block_f16", D=1, ntaps=1024, n=1048576, streams=2,
@@ -178,8 +181,10 @@ def main():
         taps = sdrhip.taps_lpf(240e3 * 147, 16e3, T, 147)
     else:
         taps = sdrhip.taps_lpf(2.4e6, 100e3, T, 1)
-    if cfg["kind"] == "mono_u8":  # src/project.cpp:263-266: the audio LPF of mode 0
+    if cfg["kind"] in ("mono_u8", "stereo_u8"):  # src/project.cpp:263-273: audio LPF (+ BPFs) of mode 0
         d_ha = torch.from_numpy(sdrhip.taps_lpf(240e3, 16e3, 101, 1)).to(dev)
+        d_hp = torch.from_numpy(sdrhip.taps_bpf(240e3, 18.5e3, 19.5e3, 101, 1)).to(dev)
+        d_hs = torch.from_numpy(sdrhip.taps_bpf(240e3, 22e3, 54e3, 101, 1)).to(dev)
     d_h = torch.from_numpy(taps).to(dev)
 
     # synthetic input generated on the device (no host traffic), then kept resident
@@ -211,6 +216,27 @@ def main():
         flops_per_unit = 2 * 2 * T / D + 10 + 2.0 * 101 / (D * down) + 1
         unit = "MS/s"
         metric = "IQ MSamples/sec through the mode-0 mono path (u8 IQ -> s16 PCM)"
+        bound = "valu"
+    elif kind == "stereo_u8":
+        D, up, down = cfg["D"], cfg["up"], cfg["down"]
+        na = sdrhip.resample_out_len(up, down, n // D)
+        z = lambda k: torch.zeros(S * k, dtype=torch.float32, device=dev)  # noqa: E731
+        sbuf = dict(delay=z(50), audio=z(100), slp=z(100), pilot=z(100), stereo=z(100),
+                    pll=torch.tensor([1, 0, 0, 0, 0, 1], dtype=torch.float32, device=dev).repeat(S))
+        taps_s = sdrhip.StereoTaps(d_h.data_ptr(), T, d_ha.data_ptr(), 101, d_hp.data_ptr(), d_hs.data_ptr(), 101)
+        state_s = sdrhip.StereoState(st0.data_ptr(), st1.data_ptr(), ns, p0.data_ptr(), p1.data_ptr(),
+                                     sbuf["delay"].data_ptr(), 50, sbuf["audio"].data_ptr(), sbuf["slp"].data_ptr(),
+                                     100, sbuf["pilot"].data_ptr(), sbuf["stereo"].data_ptr(), 100,
+                                     sbuf["pll"].data_ptr())
+        pcm = torch.empty(S * 2 * na, dtype=torch.int16, device=dev)
+        step = lambda: ctx.stereo_pcm_u8_dev(D, iq, n, S, 2 * n, up, down, 240e3, taps_s, state_s, pcm,  # noqa
+                                             2 * na)
+        units = S * n
+        bytes_per_pair = 2.0 + 4.0 * na / n
+        # front end + mono LPF + 2 BPFs + stereo LPF (2 FLOP per tap) + demod/PLL/mixer
+        flops_per_unit = 2 * 2 * T / D + 10 + (2.0 * 101 * 2 / (D * down) + 2 * 2.0 * 101 / D) + 1
+        unit = "MS/s"
+        metric = "IQ MSamples/sec through the mode-0 stereo path (u8 IQ -> interleaved s16 L/R PCM)"
         bound = "valu"
     elif kind in ("frontend_f32", "frontend_u8"):
         D = cfg["D"]

@@ -163,6 +163,60 @@ int sdr_mono_pcm_u8_dev(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs
                         float *prev_q, float *delay_state, int ns_delay, int up, int down, const float *h_audio,
                         int audio_taps, float *state_audio, int ns_audio, int16_t *pcm, long long pcm_stride);
 
+/* ----------------------------------------------- stereo back end -------- */
+/* fmPLL (src/filter.cpp:174-228) for nstreams independent streams, one lane
+ * per stream (the recurrence is sequential in time).  pll is [nstreams][6]:
+ * {feedbackI, feedbackQ, integrator, phaseEst, trigOffset, nco_state}
+ * (src/project.cpp:48-55 initial values 1, 0, 0, 0, 0, 1), updated in place.
+ * mix == NULL: out = ncoOut; else out = ncoOut * mix * 2, i.e. fmPLL fused
+ * with pointwiseMultiply (src/filter.cpp:253-266) as src/project.cpp:126
+ * applies it.  atan2/cos/sin are evaluated in double, as the reference does. */
+int sdr_fm_pll_dev(sdr_ctx *ctx, const float *in, long long n, int nstreams, long long in_stride, float freq,
+                   float Fs, float nco_scale, float phase_adjust, float norm_bw, float *pll, const float *mix,
+                   long long mix_stride, float *out, long long out_stride);
+/* pointwiseAdd/Subtract (src/filter.cpp:267-288) + interleave (:289-301) +
+ * the s16 stage of src/project.cpp:311-314: pcm[2i] = s16(mono[i] + stereo[i]),
+ * pcm[2i+1] = s16(mono[i] - stereo[i]). */
+int sdr_stereo_pcm_dev(sdr_ctx *ctx, const float *mono, const float *stereo, long long n, int nstreams,
+                       long long stride, int16_t *pcm, long long pcm_stride);
+
+/* Device taps of the stereo back end (src/project.cpp:262-273). */
+typedef struct sdr_stereo_taps {
+  const float *h_rf;     /* RF low-pass, rf_taps */
+  int rf_taps;
+  const float *h_audio;  /* audio low-pass (x up gain), audio_taps */
+  int audio_taps;
+  const float *h_pilot;  /* 18.5-19.5 kHz band-pass, bpf_taps */
+  const float *h_stereo; /* 22-54 kHz band-pass, bpf_taps */
+  int bpf_taps;
+} sdr_stereo_taps;
+
+/* Device state of the stereo back end, one row per stream
+ * (src/project.cpp:25-55: RFState, AudioState, PLLState). */
+typedef struct sdr_stereo_state {
+  float *state_i, *state_q; /* [nstreams][ns_rf] */
+  int ns_rf;
+  float *prev_i, *prev_q;   /* [nstreams] */
+  float *delay_state;       /* [nstreams][ns_delay] mono delay (num_taps/2) */
+  int ns_delay;
+  float *state_audio;       /* [nstreams][ns_audio] mono resampler */
+  float *stereo_lp_state;   /* [nstreams][ns_audio] stereo resampler */
+  int ns_audio;
+  float *pilot_state, *stereo_state; /* [nstreams][ns_bpf] */
+  int ns_bpf;
+  float *pll;               /* [nstreams][6], see sdr_fm_pll_dev */
+} sdr_stereo_state;
+
+/* The whole stereo path of src/project.cpp:72-132 + 304-314 for one block of
+ * every stream, device-resident: u8 IQ -> front end -> {delay -> mono
+ * resampler, pilot BPF -> PLL x stereo BPF -> stereo resampler} -> L/R
+ * interleaved s16 PCM (2 * audio samples per stream and block).  The PLL
+ * constants are project.cpp's (19 kHz, ncoScale 2, phaseAdjust 0, normalised
+ * bandwidth 0.01); audio_fs is the IF rate it runs at. */
+int sdr_stereo_pcm_u8_dev(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs, int nstreams, long long iq_stride,
+                          int up, int down, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
+                          int16_t *pcm, long long pcm_stride);
+
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the
  * device (counter-based, keyed by (seed, stream, sample)); used by the

@@ -211,6 +211,21 @@ class Oracle(_Lib):
         return self.pcm_s16(audio)
 
 
+    def stereo(self, D, iq, h_rf, st, up, down, h_audio, h_pilot, h_stereo, audio_fs):
+        """src/project.cpp:72-132 + 304-314 for one stereo block: u8 IQ ->
+        interleaved s16 L/R.  st: dict of float32 state arrays (i, q, prev[2],
+        delay, audio, pilot, stereo, stereo_lp, pll[6]), updated in place."""
+        I, Q = self.u8_to_planar(iq)
+        demod = self.frontend(D, I, Q, h_rf, st["i"], st["q"], st["prev"])
+        mono = self.resample(up, down, self.delay_block(demod, st["delay"]), h_audio, st["audio"])
+        pilot = self.fir_block(demod, h_pilot, st["pilot"])
+        sband = self.fir_block(demod, h_stereo, st["stereo"])
+        nco = self.fm_pll(pilot, 19e3, audio_fs, 2.0, 0.0, 0.01, st["pll"])  # src/project.cpp:100-104,123
+        slp = self.resample(up, down, self.pointwise_mul(nco, sband), h_audio, st["stereo_lp"])
+        left, right = self.pointwise_add(mono, slp), self.pointwise_sub(mono, slp)
+        return self.pcm_s16(self.interleave(left, right))
+
+
 class Reference(_Lib):
     """The reference's own src/filter.cpp, compiled (oracle/_ref)."""
 

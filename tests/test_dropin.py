@@ -201,3 +201,97 @@ def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode):
             got[s].append(out[s].copy())
     for s in range(nstreams):
         assert np.array_equal(np.concatenate(got[s]), want[s]), f"stream {s}"
+
+
+def _stereo_setup(oracle, mode):
+    rf_fs, D, audio_fs, up, down, block_bytes = MODES[mode]
+    taps = dict(rf=oracle.taps_lpf(rf_fs, 100e3, 101, 1),
+                audio=oracle.taps_lpf(audio_fs * up, 16e3, 101 * up, up),
+                pilot=oracle.taps_bpf(audio_fs, 18.5e3, 19.5e3, 101, 1),   # src/project.cpp:268-273
+                stereo=oracle.taps_bpf(audio_fs, 22e3, 54e3, 101, 1))
+    return rf_fs, D, audio_fs, up, down, block_bytes, taps
+
+
+def _stereo_state0():
+    z = lambda k: np.zeros(k, np.float32)  # noqa: E731
+    return dict(i=z(100), q=z(100), prev=z(2), delay=z(50), audio=z(100), pilot=z(100), stereo=z(100),
+                stereo_lp=z(100), pll=np.array([1, 0, 0, 0, 0, 1], np.float32))  # src/project.cpp:48-55
+
+
+def _oracle_stereo_stream(oracle, mode, data, nblocks):
+    _, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
+    st = _stereo_state0()
+    out = []
+    for b in range(nblocks):
+        iq = np.frombuffer(data[b * block_bytes:(b + 1) * block_bytes], np.uint8)
+        out.append(oracle.stereo(D, iq, taps["rf"], st, up, down, taps["audio"], taps["pilot"], taps["stereo"],
+                                 audio_fs))
+    return np.concatenate(out), st
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_oracle_stereo_chain_equals_reference_program(oracle, mode):
+    """Pins the oracle's stereo chain (front end -> mono + pilot/stereo BPFs ->
+    PLL x mixer -> stereo resampler -> L/R interleave -> s16,
+    src/project.cpp:72-132 + 304-314) to the reference program's own PCM."""
+    ref = os.path.join(REPO, "oracle", "_ref", "project_ref")
+    if not os.path.exists(ref):
+        pytest.skip("oracle/_ref/project_ref not built")
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, _, _, _, _, block_bytes, _ = _stereo_setup(oracle, mode)
+    data = fm_iq_u8(block_bytes * 3 // 2, seed=170 + mode, fs=rf_fs).tobytes()
+    want = np.frombuffer(_project(ref, mode, "stereo", data), np.int16)
+    got, _ = _oracle_stereo_stream(oracle, mode, data, 3)
+    assert len(want) == len(got) > 0
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_device_stereo_pipeline(gpu_ctx, oracle, built_lib, mode):
+    """sdr_stereo_pcm_u8_dev: independent streams x 3 blocks, u8 IQ in,
+    interleaved s16 L/R out, every byte equal to the oracle chain (pinned to
+    the reference program above), and every carried state -- including the
+    PLL's six floats -- bit-equal after each block."""
+    sdrhip = built_lib
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
+    nstreams, nblk = 3, 3
+    npairs = block_bytes // 2
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    streams = [fm_iq_u8(npairs * nblk, seed=190 + 7 * s + mode, fs=rf_fs).tobytes() for s in range(nstreams)]
+    A = sdrhip.DeviceArray
+    d_taps = {k: A.from_numpy(gpu_ctx, v) for k, v in taps.items()}
+    t = sdrhip.StereoTaps(d_taps["rf"].ptr, 101, d_taps["audio"].ptr, len(taps["audio"]), d_taps["pilot"].ptr,
+                          d_taps["stereo"].ptr, 101)
+    st0 = _stereo_state0()
+    d_st = {k: A.from_numpy(gpu_ctx, np.tile(v, nstreams)) for k, v in st0.items() if k != "prev"}
+    d_pi, d_pq = A.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32)), A.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    state = sdrhip.StereoState(d_st["i"].ptr, d_st["q"].ptr, 100, d_pi.ptr, d_pq.ptr, d_st["delay"].ptr, 50,
+                               d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr, d_st["stereo"].ptr,
+                               100, d_st["pll"].ptr)
+    pcm_stride = 2 * na + 6
+    d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
+    ost = [_stereo_state0() for _ in range(nstreams)]
+    for b in range(nblk):
+        blk = np.stack([np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
+                        for s in range(nstreams)])
+        d_iq = A.from_numpy(gpu_ctx, blk)
+        gpu_ctx.stereo_pcm_u8_dev(D, d_iq, npairs, nstreams, 2 * npairs, up, down, audio_fs, t, state, d_pcm,
+                                  pcm_stride)
+        gpu_ctx.synchronize()
+        got = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :2 * na]
+        for s in range(nstreams):
+            want = oracle.stereo(D, blk[s], taps["rf"], ost[s], up, down, taps["audio"], taps["pilot"],
+                                 taps["stereo"], audio_fs)
+            assert np.array_equal(got[s], want), f"mode {mode} stream {s} block {b}"
+        for k in ("pll", "pilot", "stereo", "stereo_lp", "audio", "delay"):
+            dev = d_st[k].download().reshape(nstreams, -1)
+            for s in range(nstreams):
+                assert_bits(dev[s], ost[s][k], f"{k} stream {s} block {b}")
+        prev = np.stack([d_pi.download(), d_pq.download()], axis=1)
+        for s in range(nstreams):
+            assert_bits(prev[s], ost[s]["prev"], f"prev stream {s} block {b}")
+
