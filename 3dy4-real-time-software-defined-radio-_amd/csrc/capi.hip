@@ -484,8 +484,11 @@ int sdr_fm_pll_dev(sdr_ctx* c, const float* in, long long n, int nstreams, long 
   if (n <= 0 || nstreams < 1) return fail(c, SDR_EINVAL, "empty block (fmPLL writes ncoOut[0], filter.cpp:186)");
   if (nstreams > 1 && (in_stride < n || out_stride < n || (mix && mix_stride < n)))
     return fail(c, SDR_EINVAL, "stream strides overlap");
+  const long long astride = (n + 1 + 3) / 4 * 4;  // trigArg per sample (+ the incoming nco_state)
+  float* args = static_cast<float*>(scratch(c, kPipe6, (size_t)nstreams * astride * sizeof(float)));
+  if (!args) return fail(c, SDR_ENOMEM, "pll argument buffer");
   hipError_t e = sdr::launch_pll(in, n, nstreams, in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix,
-                                 mix_stride, out, out_stride, c->cur);
+                                 mix_stride, out, out_stride, args, astride, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "pll launch");
   return SDR_OK;
 }

@@ -76,7 +76,8 @@ hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_str
 // with the x2 mixer; L/R + interleave + s16 output stage.
 hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
                       float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
-                      long long mix_stride, float* out, long long out_stride, hipStream_t st);
+                      long long mix_stride, float* out, long long out_stride, float* args, long long args_stride,
+                      hipStream_t st);
 hipError_t launch_stereo_pcm(const float* a, const float* b, long long n, int nstreams, long long stride,
                              int16_t* pcm, long long pcm_stride, hipStream_t st);
 hipError_t launch_synth_fm_u8(uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

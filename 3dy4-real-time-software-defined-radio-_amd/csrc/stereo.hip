@@ -7,9 +7,11 @@
 // are the FIR / resampler kernels of fir_tile.hip / resample*.hip.
 //
 // fmPLL is a sequential recurrence (each sample's phase detector reads the
-// previous sample's NCO), so it runs one lane per stream: streams are the
-// parallel axis, samples are a loop.  Arithmetic follows the reference's
-// promotions exactly: the loop filter in fp32, atan2 / cos / sin of the fp32
+// previous sample's feedback oscillator), so it runs one lane per stream:
+// streams are the parallel axis, samples are a loop; the NCO output, which
+// does not feed back, is evaluated afterwards in parallel over samples.
+// Arithmetic follows the reference's promotions exactly: the loop filter in
+// fp32, atan2 / cos / sin of the fp32
 // arguments in double (the reference calls the double C functions), every
 // result rounded back to float where the reference stores a float.
 #include "sdr_common.hpp"
@@ -22,23 +24,28 @@ namespace {
 constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
 
 // pll[6] per stream: feedbackI, feedbackQ, integrator, phaseEst, trigOffset, nco_state
-// (src/project.cpp:48-55).  mix == nullptr: out = ncoOut; else out = ncoOut * mix * 2.
+// (src/project.cpp:48-55).  Only the recurrence runs here: the phase detector
+// (atan2) and the feedback oscillator (sin/cos) of every sample depend on the
+// previous sample.  The NCO output cos(trigArg*ncoScale + phaseAdjust) does
+// not feed back, so this kernel only records trigArg (args[k+1] for sample k,
+// args[0] = the incoming nco_state) and nco_kernel evaluates all of them in
+// parallel.  The last sample's NCO becomes the new nco_state here.
 __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, long long n, int nstreams,
                                                  long long in_stride, float freq, float Fs, float nco_scale,
                                                  float phase_adjust, float norm_bw, float* __restrict__ pll,
-                                                 const float* __restrict__ mix, long long mix_stride,
-                                                 float* __restrict__ out, long long out_stride) {
+                                                 float* __restrict__ args, long long args_stride) {
   const int s = blockIdx.x * 64 + threadIdx.x;
   if (s >= nstreams) return;
   const float* x = in + (long long)s * in_stride;
-  const float* m = mix ? mix + (long long)s * mix_stride : nullptr;
-  float* y = out + (long long)s * out_stride;
+  float* ar = args + (long long)s * args_stride;
   float* st = pll + 6LL * s;
-  float fbI = st[0], fbQ = st[1], integrator = st[2], phaseEst = st[3], trigOffset = st[4], nco_prev = st[5];
+  float fbI = st[0], fbQ = st[1], integrator = st[2], phaseEst = st[3], trigOffset = st[4];
+  ar[0] = st[5];  // ncoOut[0] = nco_state (src/filter.cpp:186)
   // src/filter.cpp:175-179: float Cp = 2.666, Ci = 3.555; Kp, Ki in float
   const float Kp = norm_bw * 2.666f;
   const float Ki = norm_bw * norm_bw * 3.555f;
   const double step = 2.0 * kPiD * (double)(freq / Fs);  // 2*PI*(freq/Fs), double (PI is a double literal)
+  float arg = 0.0f;
   for (long long k = 0; k < n; ++k) {
     const float v = x[k];
     const float eI = (v == 0.0f ? 1.0f : v) * fbI;
@@ -47,20 +54,33 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     integrator = integrator + Ki * eD;
     phaseEst = phaseEst + (Kp * eD + integrator);
     trigOffset = trigOffset + 1.0f;
-    const float arg = (float)(step * (double)trigOffset + (double)phaseEst);
-    fbI = (float)cos((double)arg);
-    fbQ = (float)sin((double)arg);
-    const float nco = (float)cos((double)(arg * nco_scale + phase_adjust));
-    // ncoOut[k] is the previous sample's NCO (ncoOut[0] = nco_state, :186)
-    y[k] = m ? nco_prev * m[k] * 2.0f : nco_prev;
-    nco_prev = nco;
+    arg = (float)(step * (double)trigOffset + (double)phaseEst);
+    double sv, cv;
+    sincos((double)arg, &sv, &cv);  // one argument reduction for both (same values as sin() and cos())
+    fbI = (float)cv;
+    fbQ = (float)sv;
+    if (k + 1 < n) ar[k + 1] = arg;
   }
   st[0] = fbI;
   st[1] = fbQ;
   st[2] = integrator;
   st[3] = phaseEst;
   st[4] = trigOffset;
-  st[5] = nco_prev;  // nco_state = the last sample's NCO (:221-222)
+  st[5] = (float)cos((double)(arg * nco_scale + phase_adjust));  // nco_state (:221-222)
+}
+
+// ncoOut[k] from the recorded arguments (k = 0: the old nco_state), optionally
+// mixed: out = ncoOut * mix * 2 (pointwiseMultiply's gain, src/filter.cpp:264).
+__global__ __launch_bounds__(kWG) void nco_kernel(const float* __restrict__ args, long long args_stride, long long n,
+                                                  float nco_scale, float phase_adjust, const float* __restrict__ mix,
+                                                  long long mix_stride, float* __restrict__ out,
+                                                  long long out_stride) {
+  const int s = blockIdx.y;
+  const long long k = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (k >= n) return;
+  const float a = args[(long long)s * args_stride + k];
+  const float nco = k == 0 ? a : (float)cos((double)(a * nco_scale + phase_adjust));
+  out[(long long)s * out_stride + k] = mix ? nco * mix[(long long)s * mix_stride + k] * 2.0f : nco;
 }
 
 // L/R + interleave + s16: pcm[2i] = q(a[i] + b[i]), pcm[2i+1] = q(a[i] - b[i])
@@ -81,9 +101,14 @@ __global__ __launch_bounds__(kWG) void stereo_pcm_kernel(const float* __restrict
 
 hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
                       float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
-                      long long mix_stride, float* out, long long out_stride, hipStream_t st) {
+                      long long mix_stride, float* out, long long out_stride, float* args, long long args_stride,
+                      hipStream_t st) {
   hipLaunchKernelGGL(pll_kernel, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams, in_stride,
-                     freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix, mix_stride, out, out_stride);
+                     freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(nco_kernel, dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0, st, args,
+                     args_stride, n, nco_scale, phase_adjust, mix, mix_stride, out, out_stride);
   return hipGetLastError();
 }
 
