@@ -217,6 +217,86 @@ int sdr_dev_memset(sdr_ctx* c, void* dst, int value, size_t bytes) {
   return SDR_OK;
 }
 
+// Pinned host memory, stream-ordered copies and events: what a streaming
+// host program needs to overlap its I/O with the device work (the block
+// pipeline of host/sdr_project.cpp).
+int sdr_host_alloc(sdr_ctx* c, size_t bytes, void** ptr) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!ptr) return fail(c, SDR_EINVAL, "null ptr");
+  *ptr = nullptr;
+  hipError_t e = hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(c, SDR_ENOMEM, "hipHostMalloc %zu", bytes)
+                                                       : hip_fail(c, e, "hipHostMalloc");
+  return SDR_OK;
+}
+
+int sdr_host_free(sdr_ctx* c, void* ptr) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (ptr) SDR_HIP(c, hipHostFree(ptr));
+  return SDR_OK;
+}
+
+int sdr_copy_h2d_async(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->cur));
+  return SDR_OK;
+}
+
+int sdr_copy_d2h_async(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
+  int rc = enter(c);
+  if (rc) return rc;
+  SDR_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->cur));
+  return SDR_OK;
+}
+
+struct sdr_event {
+  hipEvent_t ev = nullptr;
+};
+
+int sdr_event_create(sdr_ctx* c, sdr_event** ev) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!ev) return fail(c, SDR_EINVAL, "null event");
+  auto* e = new sdr_event;
+  hipError_t h = hipEventCreateWithFlags(&e->ev, hipEventDisableTiming);
+  if (h != hipSuccess) {
+    delete e;
+    return hip_fail(c, h, "hipEventCreate");
+  }
+  *ev = e;
+  return SDR_OK;
+}
+
+int sdr_event_record(sdr_ctx* c, sdr_event* ev) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!ev) return fail(c, SDR_EINVAL, "null event");
+  SDR_HIP(c, hipEventRecord(ev->ev, c->cur));
+  return SDR_OK;
+}
+
+int sdr_event_synchronize(sdr_ctx* c, sdr_event* ev) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!ev) return fail(c, SDR_EINVAL, "null event");
+  SDR_HIP(c, hipEventSynchronize(ev->ev));
+  return SDR_OK;
+}
+
+int sdr_event_destroy(sdr_ctx* c, sdr_event* ev) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (ev) {
+    hipError_t h = hipEventDestroy(ev->ev);
+    delete ev;
+    if (h != hipSuccess) return hip_fail(c, h, "hipEventDestroy");
+  }
+  return SDR_OK;
+}
+
 // ------------------------------------------------------------ taps (host) --
 // Windowed-sinc design, src/filter.cpp:14-49: the sinc in double, stored to
 // float, then widened again for the sin^2 window and the up-factor gain.

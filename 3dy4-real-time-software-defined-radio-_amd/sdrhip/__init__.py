@@ -57,6 +57,14 @@ _SIGS = {
     "sdr_copy_h2d": [_vp, _vp, _vp, C.c_size_t],
     "sdr_copy_d2h": [_vp, _vp, _vp, C.c_size_t],
     "sdr_dev_memset": [_vp, _vp, _i, C.c_size_t],
+    "sdr_host_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
+    "sdr_host_free": [_vp, _vp],
+    "sdr_copy_h2d_async": [_vp, _vp, _vp, C.c_size_t],
+    "sdr_copy_d2h_async": [_vp, _vp, _vp, C.c_size_t],
+    "sdr_event_create": [_vp, C.POINTER(_vp)],
+    "sdr_event_record": [_vp, _vp],
+    "sdr_event_synchronize": [_vp, _vp],
+    "sdr_event_destroy": [_vp, _vp],
     "sdr_resample_out_len": [_i, _i, _ll],
     "sdr_taps_lpf": [C.c_float, C.c_float, _i, _i, _vp],
     "sdr_taps_bpf": [C.c_float, C.c_float, C.c_float, _i, _i, _vp],

@@ -75,6 +75,19 @@ int sdr_copy_h2d(sdr_ctx *ctx, void *dst, const void *src, size_t bytes); /* syn
 int sdr_copy_d2h(sdr_ctx *ctx, void *dst, const void *src, size_t bytes); /* synchronous */
 int sdr_dev_memset(sdr_ctx *ctx, void *dst, int value, size_t bytes);   /* stream-ordered */
 
+/* Pinned host buffers, stream-ordered copies and events, for callers that
+ * overlap their own I/O with the device work (host/sdr_project.cpp: the
+ * HIP-stream replacement of src/project.cpp's per-block threads + queue). */
+typedef struct sdr_event sdr_event;
+int sdr_host_alloc(sdr_ctx *ctx, size_t bytes, void **ptr); /* page-locked */
+int sdr_host_free(sdr_ctx *ctx, void *ptr);
+int sdr_copy_h2d_async(sdr_ctx *ctx, void *dst, const void *src, size_t bytes); /* stream-ordered */
+int sdr_copy_d2h_async(sdr_ctx *ctx, void *dst, const void *src, size_t bytes); /* stream-ordered */
+int sdr_event_create(sdr_ctx *ctx, sdr_event **ev);
+int sdr_event_record(sdr_ctx *ctx, sdr_event *ev);      /* marks the work enqueued so far */
+int sdr_event_synchronize(sdr_ctx *ctx, sdr_event *ev); /* blocks until that work is done */
+int sdr_event_destroy(sdr_ctx *ctx, sdr_event *ev);
+
 /* --------------------------------------------------- coefficient design -- */
 /* impulseResponseLPF / impulseResponseBPF, src/filter.cpp:14-49
  * (filter.h:17, :27): windowed-sinc taps with the up-factor gain folded in,

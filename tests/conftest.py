@@ -42,8 +42,8 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def built_lib():
-    """libsdrhip.so + libdy4filter_hip.so, built in-tree if missing."""
-    if not (os.path.exists(os.path.join(PKG, "libsdrhip.so")) and os.path.exists(os.path.join(PKG, "libdy4filter_hip.so"))):
+    """libsdrhip.so + libdy4filter_hip.so + sdr_project, built in-tree if missing."""
+    if not all(os.path.exists(os.path.join(PKG, f)) for f in ("libsdrhip.so", "libdy4filter_hip.so", "sdr_project")):
         _make(PKG, "-j4")
     import sdrhip
 

@@ -126,3 +126,17 @@ def test_c_example_runs(built_lib, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-1000:]
     assert r.stdout.startswith("ok ")
+
+
+def test_sdr_project_usage_without_gpu(built_lib):
+    """host/sdr_project keeps src/project.cpp:155-176's command line: wrong
+    argument counts print the usage and exit 1, a mode above 3 is refused --
+    both before any device is touched (so this runs on CPU)."""
+    import subprocess
+
+    prog = os.path.join(PKG, "sdr_project")
+    r = subprocess.run([prog], capture_output=True)
+    assert r.returncode == 1 and b"<mode> <mono/stereo>" in r.stderr
+    r = subprocess.run([prog, "7", "mono"], capture_output=True)
+    assert r.returncode == 1 and b"Wrong mode: 7" in r.stderr
+
