@@ -332,11 +332,12 @@ hipError_t launch_resample(int up, int down, const float* x, long long n, int ns
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
                            long long ny, float* scratch_taps, hipStream_t st) {
   {
-    // the sliding-window kernel (resample_rs.hip) first, for the shapes it covers
+    // resample_rs.hip's kernels first (lane-phase, then sliding-window), for the shapes they cover
     hipError_t e = hipSuccess;
+    bool state_done = false;
     if (launch_resample_rs(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, scratch_taps,
-                           st, &e)) {
-      if (e != hipSuccess || ns <= 0) return e;
+                           st, &e, &state_done)) {
+      if (e != hipSuccess || ns <= 0 || state_done) return e;
       hipLaunchKernelGGL(resample_commit, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st, x, n,
                          x_stride, state, ns);
       return hipGetLastError();

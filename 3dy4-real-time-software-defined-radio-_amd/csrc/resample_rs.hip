@@ -315,10 +315,10 @@ constexpr int kLpBuf = 19456;  // floats per staging buffer (76 KiB); two buffer
 struct LpArgs {
   const float* x;
   long long n, x_stride;
-  const float* hs;   // [4][L][U] shifted taps (build_shifted)
-  const int* lanes;  // [kLpSlots]: phi | sub << 16, or -1
+  const float* hs;   // [4][L][U] taps pre-shifted by A (build_lp_tables)
+  const int* lanes;  // [kLpSlots]: phi | sub << 16, or -1 (build_lp_tables)
   int up, down;
-  const float* state;
+  float* state;      // read by each stream's first item, then rewritten by it
   int ns;
   float* y;
   long long y_stride, ny;
@@ -337,17 +337,20 @@ __constant__ unsigned char kB128Groups[4][16] = {
     {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
     {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
 
-// One workgroup: counting sort of the L*S items by bank class, then deal.
-__global__ __launch_bounds__(kLpSlots) void build_lanes(int up, int down, int S, int base0, int* lanes) {
-  __shared__ int cnt[16], start[16], fill[16];
-  __shared__ int order[kLpSlots];
+// Every workgroup builds the lane table itself (448 items, LDS atomics):
+// counting sort of the L*S items by bank class, then deal round-robin over
+// the 28 lane groups.  Which lane gets which item does not change any
+// output bit (each output is computed by exactly one lane, in the same
+// order), so the atomics' nondeterminism is harmless.
+__device__ __forceinline__ int lp_lane_code(int up, int down, int S, int base0, int* cnt, int* start, int* fill,
+                                            int* order, int* codes) {
   const int t = threadIdx.x;
   const int nit = up * S;
   if (t < 16) {
     cnt[t] = 0;
     fill[t] = 0;
   }
-  lanes[t] = -1;
+  codes[t] = -1;
   __syncthreads();
   int cls = -1;
   if (t < nit) {
@@ -371,9 +374,30 @@ __global__ __launch_bounds__(kLpSlots) void build_lanes(int up, int down, int S,
     // position r in class order -> group r mod 28, member r / 28
     const int g = t % kLpGroups, m = t / kLpGroups;
     const int item = order[t];
-    const int lane = (g >> 2) * 64 + kB128Groups[g & 3][m];
-    lanes[lane] = (item % up) | ((item / up) << 16);
+    codes[(g >> 2) * 64 + kB128Groups[g & 3][m]] = (item % up) | ((item / up) << 16);
   }
+  __syncthreads();
+  return codes[t];
+}
+
+// One launch for both tables of resample_lp: blocks 0..G-2 write the shifted
+// rows hs[A][p][u] = h[p + (u + A - 3) * L] (0 where u + A - 3 is outside
+// [0, CMAX)), the last block builds the lane table.
+__global__ __launch_bounds__(kLpSlots) void build_lp_tables(const float* __restrict__ h, int up, int down, int cmax,
+                                                            int U, int S, int base0, float* __restrict__ hs,
+                                                            int* __restrict__ lanes) {
+  if (blockIdx.x == gridDim.x - 1) {
+    __shared__ int cnt[16], start[16], fill[16], order[kLpSlots], codes[kLpSlots];
+    lanes[threadIdx.x] = lp_lane_code(up, down, S, base0, cnt, start, fill, order, codes);
+    return;
+  }
+  const long long idx = (long long)blockIdx.x * kLpSlots + threadIdx.x;
+  if (idx >= 4LL * up * U) return;
+  const int u = (int)(idx % U);
+  const int p = (int)((idx / U) % up);
+  const int A = (int)(idx / ((long long)U * up));
+  const int i = u + A - 3;
+  hs[idx] = (i >= 0 && i < cmax) ? h[p + (long long)i * up] : 0.0f;
 }
 
 // Stage item `it` (its whole input span) into buf: LDS-DMA for the chunks
@@ -483,10 +507,17 @@ template <int CMAX, int K>
 __global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
   __shared__ __attribute__((aligned(16))) float bufA[kLpBuf];
   __shared__ __attribute__((aligned(16))) float bufB[kLpBuf];
+  __shared__ float cbuf[kLpSlots];  // the new state, in flight during the compute
   constexpr int U = (CMAX + 6) / 4 * 4;
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-  // this lane's item and taps, for the whole launch
+  // items: contiguous range per workgroup
+  const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
+  if (i0 >= i1) return;
+  // the first item's DMA runs while this lane's item and taps are loaded
+  if (a.ablate != 1) lp_stage<CMAX>(a, bufA, i0, wv, ln);
   const int code = a.lanes[threadIdx.x];
   const bool valid = code >= 0;
   const int phi = valid ? (code & 0xffff) : 0, sub = valid ? (code >> 16) : 0;
@@ -503,15 +534,17 @@ __global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
     tp[u + 2] = v.z;
     tp[u + 3] = v.w;
   }
-  // items: contiguous range per workgroup
-  const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
-  const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
-  const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
-  if (i0 >= i1) return;
-  if (a.ablate != 1) lp_stage<CMAX>(a, bufA, i0, wv, ln);
   for (int it = i0; it < i1; ++it) {
     dma_drain();
     __syncthreads();  // item it's span has landed; the other buffer is free
+    // the stream's first item is the only reader of its old state and its span
+    // is staged now: state <- last ns inputs of the block (src/filter.cpp:169),
+    // brought into LDS by DMA during the compute and stored after it
+    // (ns <= kLpSlots on this path)
+    const bool commit = it % a.nbat == 0;
+    if (commit && (int)threadIdx.x < a.ns)
+      __builtin_amdgcn_global_load_lds(a.x + (long long)(it / a.nbat) * a.x_stride + (a.n - a.ns) + threadIdx.x,
+                                       cbuf + wv * 64, 4, 0, 0);
     const bool odd = ((it - i0) & 1) != 0;
     if (it + 1 < i1 && a.ablate != 1) {
       if (odd)
@@ -524,6 +557,10 @@ __global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
         lp_compute<CMAX, K>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
       else
         lp_compute<CMAX, K>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
+    }
+    if (commit && (int)threadIdx.x < a.ns) {
+      dma_drain();
+      a.state[(long long)(it / a.nbat) * a.ns + threadIdx.x] = cbuf[threadIdx.x];
     }
   }
 }
@@ -545,14 +582,15 @@ bool rs_enabled() {
 size_t resample_rs_scratch_floats(int up, int ntaps) {
   const int cmax = (ntaps + up - 1) / up;
   const int U = (cmax + 3 + 3) / 4 * 4;
-  return (size_t)4 * up * U + kLpSlots;  // shifted rows + the lane table of resample_lp
+  return (size_t)4 * up * U + kLpSlots;  // shifted rows (+ resample_lp's lane table)
 }
 
 // Returns false (nothing launched) when the shape is not one this kernel
 // covers; the caller then takes the phase-major kernel of resample.hip.
 bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
-                        float* scratch, hipStream_t st, hipError_t* err) {
+                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done) {
+  *state_done = false;
   const int cmax = (ntaps + up - 1) / up;
   if (up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
   // 16-B chunks straight from the rows
@@ -561,20 +599,11 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   const int base0 = -(((cmax - 1) + 3) / 4 * 4);
   const int qmax = (int)((long long)(up - 1) * down / up);
   const bool use_lp = lp_enabled() && up <= kLpSlots && (long long)up * down < (1LL << 31) &&
-                      qmax + 1 - base0 + 4 <= kLpBuf;
+                      qmax + 1 - base0 + 4 <= kLpBuf && ns <= kLpSlots;
   // resample_rs: the ring must hold a group's whole window plus the next group's new inputs
   const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
   const long long step = ((long long)kRsPG * down + up - 1) / up + 8;
   if (!use_lp && (!rs_enabled() || span + step > kRsRing)) return false;
-  const int U = (cmax + 3 + 3) / 4 * 4;
-  const long long tab = 4LL * up * U;
-  hipLaunchKernelGGL(build_shifted, dim3((unsigned)((tab + kWG - 1) / kWG)), dim3(kWG), 0, st, h, ntaps, up, cmax, U,
-                     scratch);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    *err = e;
-    return true;
-  }
   static const int ablate = [] {
     const char* v = std::getenv("SDR_ABLATE");
     return v ? std::atoi(v) : 0;
@@ -601,7 +630,7 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       b.n = n;
       b.x_stride = x_stride;
       b.hs = scratch;
-      b.lanes = reinterpret_cast<int*>(scratch + tab);
+      b.lanes = reinterpret_cast<const int*>(scratch + 4LL * up * ((cmax + 6) / 4 * 4));
       b.up = up;
       b.down = down;
       b.state = state;
@@ -615,7 +644,11 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       b.nitems = b.nbat * nstreams;
       b.S = S;
       b.ablate = ablate;
-      hipLaunchKernelGGL(build_lanes, dim3(1), dim3(kLpSlots), 0, st, up, down, S, base0, const_cast<int*>(b.lanes));
+      const int U = (cmax + 6) / 4 * 4;
+      const long long tab = 4LL * up * U;
+      hipLaunchKernelGGL(build_lp_tables, dim3((unsigned)((tab + kLpSlots - 1) / kLpSlots + 1)), dim3(kLpSlots), 0, st,
+                         h, up, down, cmax, U, S, base0, scratch, const_cast<int*>(b.lanes));
+      if ((*err = hipGetLastError()) != hipSuccess) return true;
       const int grid = b.nitems < ncu ? b.nitems : ncu;
       if (cmax == 151) {
         if (K == 4)
@@ -629,8 +662,18 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
           hipLaunchKernelGGL((resample_lp<101, 7>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
       }
       *err = hipGetLastError();
+      *state_done = true;  // resample_lp commits the state itself
       return true;
     }
+  }
+  const int U = (cmax + 3 + 3) / 4 * 4;
+  const long long tab = 4LL * up * U;
+  hipLaunchKernelGGL(build_shifted, dim3((unsigned)((tab + kWG - 1) / kWG)), dim3(kWG), 0, st, h, ntaps, up, cmax, U,
+                     scratch);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    *err = e;
+    return true;
   }
   RsArgs a;
   a.x = x;

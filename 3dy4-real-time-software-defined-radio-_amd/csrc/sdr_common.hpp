@@ -117,6 +117,6 @@ size_t resample_scratch_floats(int up, int ntaps);
 size_t resample_rs_scratch_floats(int up, int ntaps);
 bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
-                        float* scratch, hipStream_t st, hipError_t* err);
+                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done);
 
 }  // namespace sdr

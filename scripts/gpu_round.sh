@@ -29,6 +29,13 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/
 rc=$?; echo "rocprof rc=$rc"; find "$OUT/prof" -name '*stats*' | head
 [ $rc -eq 0 ] || exit $rc
 
+# per-config kernel statistics (the other configs' dominant kernels)
+for cfg in ${PROF_CFGS:-}; do
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof_$cfg" -o bench \
+    -- python3 bench.py --config "$cfg" --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof_bench_$cfg.json" 2>> "$OUT/prof.err"
+  rc=$?; echo "rocprof $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+
 # HBM traffic: one counter per pass (FETCH_SIZE, then WRITE_SIZE)
 if [ -n "${PMC:-}" ]; then
   for ctr in FETCH_SIZE WRITE_SIZE; do
@@ -38,5 +45,13 @@ if [ -n "${PMC:-}" ]; then
   done
   python scripts/pmc_traffic.py "$(find $OUT/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1)" \
     "$(find $OUT/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)" fir_tile "$OUT/traffic_cfg2.json"
+  # the resampler's traffic (cfg3)
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc3_$ctr" -o pmc \
+      -- python3 bench.py --config cfg3 --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2>> "$OUT/prof.err"
+    rc=$?; echo "pmc cfg3 $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  python scripts/pmc_traffic.py "$(find $OUT/pmc3_FETCH_SIZE -name '*counter_collection.csv' | head -1)" \
+    "$(find $OUT/pmc3_WRITE_SIZE -name '*counter_collection.csv' | head -1)" resample_lp "$OUT/traffic_cfg3.json"
 fi
 exit 0
