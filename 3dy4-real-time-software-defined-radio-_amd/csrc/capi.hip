@@ -17,6 +17,7 @@ struct sdr_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
+  int arith = SDR_ARITH_EXACT;
   // grow-only device scratch for the host-pointer wrappers and internal use
   void* buf[17] = {};
   size_t cap[17] = {};
@@ -169,6 +170,13 @@ int sdr_ctx_set_stream(sdr_ctx* c, void* s) {
 }
 
 void* sdr_ctx_get_stream(sdr_ctx* c) { return c ? static_cast<void*>(c->cur) : nullptr; }
+
+int sdr_ctx_set_arith(sdr_ctx* c, int mode) {
+  if (!c) return SDR_EINVAL;
+  if (mode != SDR_ARITH_EXACT && mode != SDR_ARITH_FMA) return fail(c, SDR_EINVAL, "unknown arithmetic mode %d", mode);
+  c->arith = mode;
+  return SDR_OK;
+}
 
 int sdr_ctx_synchronize(sdr_ctx* c) {
   int rc = enter(c);
@@ -413,6 +421,7 @@ static int frontend_dev(sdr_ctx* c, sdr::Src src, int D, const float* I, const f
   a.prev1 = prev_q;
   a.out = demod;
   a.out_stride = out_stride;
+  a.fma = c->arith == SDR_ARITH_FMA;
   bool fast;
   if (src == sdr::Src::F32)
     fast = vec_ok(I, x_stride, 4, nstreams) && vec_ok(Q, x_stride, 4, nstreams);

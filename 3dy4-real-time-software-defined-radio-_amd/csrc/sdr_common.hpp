@@ -44,6 +44,7 @@ struct FirLaunch {
   int tiles_per_wg;  // persistent tile kernels: tiles per workgroup
   int walk;          // 0: each workgroup walks contiguous tiles; 1: XCD-strided (see fir_tile.hip)
   int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math, 3 = no output stores
+  int fma;           // SDR_ARITH_FMA: fused multiply-add FIR arithmetic where a fast path implements it
 };
 
 // Exact reference conversion of one wire byte, src/iofunc.cpp:118:
@@ -106,6 +107,10 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
                              void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
                              hipStream_t st);
 hipError_t launch_f32_to_f16(const float* x, long long count, void* y, hipStream_t st);
+
+// Loader/consumer front-end engine (fir_stream.hip): fused f32 D = 10, T = 101.
+bool fir_stream_ok(int D, int ntaps, int ns, bool demod, int nch, Src src);
+hipError_t launch_fir_stream(const FirLaunch& a, const float* h, hipStream_t st);
 
 // Whether the tiled fast path handles (D, ntaps, ns) for this source; false
 // means launch_fir takes the generic path (still exact, slower).

@@ -33,6 +33,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 HEADER_PATH = os.path.join(REPO_DIR, "include", "sdr_hip.h")
 
 SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_ENODEV = 0, -1, -2, -3, -4
+ARITH_EXACT, ARITH_FMA = 0, 1  # sdr_ctx_set_arith modes
 
 _lib = None
 
@@ -51,6 +52,7 @@ _SIGS = {
     "sdr_ctx_set_stream": [_vp, _vp],
     "sdr_ctx_get_stream": [_vp],
     "sdr_ctx_synchronize": [_vp],
+    "sdr_ctx_set_arith": [_vp, _i],
     "sdr_ctx_last_error": [_vp],
     "sdr_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "sdr_dev_free": [_vp, _vp],
@@ -213,6 +215,11 @@ class Context:
 
     def __exit__(self, *exc):
         self.close()
+
+    def set_arith(self, mode: int):
+        """FIR arithmetic of the fused front end: ARITH_EXACT (the reference's
+        bits, default) or ARITH_FMA (one fused multiply-add per tap)."""
+        self._check(lib().sdr_ctx_set_arith(self._c, mode), "set_arith")
 
     def set_stream(self, hip_stream: int | None):
         """Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""

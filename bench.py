@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--arith", choices=("exact", "fma"), default=os.environ.get("SDR_BENCH_ARITH", "exact"),
+                    help="front-end FIR arithmetic: the reference's bits (exact) or one fused multiply-add per tap "
+                         "(fma, tolerance-tested)")
     return ap.parse_args()
 
 
@@ -172,6 +175,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
+    ctx.set_arith(sdrhip.ARITH_FMA if args.arith == "fma" else sdrhip.ARITH_EXACT)
 
     S, n, T = cfg["streams"], cfg["n"], cfg["ntaps"]
     seed = 1234 + 7919 * rank
@@ -363,7 +367,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": cfg["workload"], "streams_per_gpu": S, "pairs_per_stream_per_step": n,
                        "ntaps": T, "parallelism": f"{world} GPU(s) x independent streams, no data-path collective",
-                       "state_carried_across_steps": True},
+                       "state_carried_across_steps": True,
+                       "arith": ("fma: one fused multiply-add per tap, tolerance-tested (DESIGN.md 2)"
+                                 if args.arith == "fma" else "exact: the reference's bits")},
             "roofline": roof, "cpu_baseline": cpu,
             **({"tolerance": tolerance} if tolerance else {}),
             "wall_ms": round(ms_wall, 3),

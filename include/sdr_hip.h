@@ -68,6 +68,16 @@ void *sdr_ctx_get_stream(sdr_ctx *ctx);
 int sdr_ctx_synchronize(sdr_ctx *ctx);
 const char *sdr_ctx_last_error(sdr_ctx *ctx);
 
+/* FIR arithmetic of the fused front end (sdr_frontend_*_dev and the calls
+ * built on it).  SDR_ARITH_EXACT (default): every product and sum rounded
+ * separately in the reference's order -- the bits of src/filter.cpp:123-140.
+ * SDR_ARITH_FMA: the same taps in the same order with one fused
+ * multiply-add per tap (one rounding instead of two); no reference
+ * counterpart, outputs within the fp32 tolerance of DESIGN.md section 2. */
+#define SDR_ARITH_EXACT 0
+#define SDR_ARITH_FMA 1
+int sdr_ctx_set_arith(sdr_ctx *ctx, int mode);
+
 /* Device memory helpers so a C/C++ caller needs no HIP headers. */
 int sdr_dev_alloc(sdr_ctx *ctx, size_t bytes, void **ptr);
 int sdr_dev_free(sdr_ctx *ctx, void *ptr);

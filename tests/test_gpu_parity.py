@@ -278,6 +278,67 @@ def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, src, D, n):
         assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), "prev_q")
 
 
+@pytest.mark.parametrize("src", ["f32", "u8"])
+@pytest.mark.parametrize("D,n", [(10, 65540), (5, 40960)])
+def test_frontend_fma_tolerance(gpu_ctx, oracle, built_lib, src, D, n):
+    """SDR_ARITH_FMA: one fused multiply-add per tap, same taps and order.  Not
+    the reference's bits; bar: demod within 1e-5 of the exact
+    oracle where I^2+Q^2 >= 1e-3, carried prev_* within 4e-6*sum|h|*max|x|,
+    state exact.  Three consecutive blocks, so the FMA prev_* feeds the next."""
+    sdrhip = built_lib
+    nstreams, nblk = 4, 3
+    h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
+    fir_tol = 4e-6 * np.abs(h).sum() * 1.0  # |x| <= 1 (u8 wire scale)
+    iq = _fm_streams(nstreams, n * nblk, seed=40)
+    nout = n // D
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    z = lambda k: sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(k, np.float32))  # noqa: E731
+    d_si, d_sq, d_pi, d_pq = z(nstreams * 100), z(nstreams * 100), z(nstreams), z(nstreams)
+    d_out = sdrhip.DeviceArray(gpu_ctx, nstreams * nout * 4)
+    ors = [dict(si=np.zeros(100, np.float32), sq=np.zeros(100, np.float32), prev=np.zeros(2, np.float32))
+           for _ in range(nstreams)]
+    gpu_ctx.set_arith(sdrhip.ARITH_FMA)
+    try:
+        worst = 0.0
+        for b in range(nblk):
+            blk = iq[:, 2 * n * b:2 * n * (b + 1)]
+            if src == "u8":
+                d_iq = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.ascontiguousarray(blk))
+                gpu_ctx.frontend_u8_dev(D, d_iq, n, nstreams, 2 * n, d_h, len(h), d_si, d_sq, 100, d_pi, d_pq, d_out,
+                                        nout)
+            else:
+                I = np.stack([oracle.u8_to_planar(blk[s])[0] for s in range(nstreams)])
+                Q = np.stack([oracle.u8_to_planar(blk[s])[1] for s in range(nstreams)])
+                gpu_ctx.frontend_dev(D, sdrhip.DeviceArray.from_numpy(gpu_ctx, I),
+                                     sdrhip.DeviceArray.from_numpy(gpu_ctx, Q), n, nstreams, n, d_h, len(h), d_si,
+                                     d_sq, 100, d_pi, d_pq, d_out, nout)
+            gpu_ctx.synchronize()
+            got = d_out.download().reshape(nstreams, nout)
+            for s in range(nstreams):
+                Is, Qs = oracle.u8_to_planar(blk[s])
+                yi = oracle.fir_decim(D, Is, h, ors[s]["si"])
+                yq = oracle.fir_decim(D, Qs, h, ors[s]["sq"])
+                env = yi.astype(np.float64) ** 2 + yq.astype(np.float64) ** 2
+                want = oracle.fm_demod(yi, yq, ors[s]["prev"])
+                # the bar holds where the discriminator is conditioned: a block's
+                # first outputs see the zero initial state (I^2+Q^2 ~ 1e-6)
+                ok = env >= 1e-3
+                assert ok.mean() > 0.99
+                err = np.abs(got[s].astype(np.float64) - want)[ok]
+                assert np.isfinite(got[s]).all()
+                assert err.max() <= 1e-5, f"stream {s} block {b}: demod max err {err.max():.3g}"
+                worst = max(worst, err.max())
+            assert_bits(d_si.download().reshape(nstreams, 100), np.stack([o["si"] for o in ors]), "state_i")
+            assert_bits(d_sq.download().reshape(nstreams, 100), np.stack([o["sq"] for o in ors]), "state_q")
+            pi = d_pi.download()
+            assert np.abs(pi - np.array([o["prev"][0] for o in ors])).max() <= fir_tol, "prev_i"
+            pq = d_pq.download()
+            assert np.abs(pq - np.array([o["prev"][1] for o in ors])).max() <= fir_tol, "prev_q"
+        print(f"fma {src} D={D}: worst demod |err| vs exact {worst:.3g}")
+    finally:
+        gpu_ctx.set_arith(sdrhip.ARITH_EXACT)
+
+
 def test_fir_decim_batched_misaligned_stride(gpu_ctx, oracle, built_lib):
     """A stride that breaks 16-B row alignment takes the generic kernel: same bits."""
     sdrhip = built_lib
