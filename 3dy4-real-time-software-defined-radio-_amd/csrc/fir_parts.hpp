@@ -1,10 +1,13 @@
-// fir_parts.hpp -- device building blocks shared by the front-end tile
-// kernels (fir_tile.hip: register-staged tiles; fir_stream.hip: loader /
-// consumer waves over an LDS-DMA ring).  Internal to libsdrhip.so.
+// fir_parts.hpp -- device building blocks of the opt-in loader/consumer
+// front end (fir_stream.hip: loader / consumer waves over an LDS-DMA ring).
+// Internal to libsdrhip.so.  The default register-staged tile kernel
+// (fir_tile.hip) keeps its own copy of the geometry: a shared-header
+// refactor of it measured 2-8 % slower on cfg2 (same-box A/B)
+// and was rolled back.
 //
 // Arithmetic contract (bit-exact with the compiled reference): see
-// fir_tile.hip.  Everything here is header-only device code; each kernel
-// TU includes it inside its own anonymous namespace.
+// fir_tile.hip.  Header-only device code; a kernel TU includes it inside
+// its own anonymous namespace.
 #pragma once
 
 #include <type_traits>
@@ -12,6 +15,16 @@
 #include "sdr_common.hpp"
 
 #pragma clang fp contract(off)
+
+// Build switches for same-box A/B (scripts/build_ab_tree.sh):
+// SDR_STAGE_PIN: pin the issue order of a tile's staging loads;
+// SDR_EDGE_DRAIN: retire the edge loads at the end of edge_fill().
+#ifndef SDR_STAGE_PIN
+#define SDR_STAGE_PIN 1
+#endif
+#ifndef SDR_EDGE_DRAIN
+#define SDR_EDGE_DRAIN 1
+#endif
 
 namespace sdr {
 namespace {
@@ -210,16 +223,16 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
   // issue a tile's loads in the same order, so hipcc's waitcnt pass merges
   // equal histories at the loop head and waits for exactly the tile being
   // staged, not for the prefetch behind it.
-  __builtin_amdgcn_sched_barrier(0);
+  if (SDR_STAGE_PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int it = 0; it < G::FULL; ++it) {
     load4(tid + it * G::NTH, v0[it], v1[it]);
-    __builtin_amdgcn_sched_barrier(0);
+    if (SDR_STAGE_PIN) __builtin_amdgcn_sched_barrier(0);
   }
   // ragged last row: clamp the index (a redundant load) so every register
   // is defined and the arrays stay in VGPRs
   if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
-  __builtin_amdgcn_sched_barrier(0);
+  if (SDR_STAGE_PIN) __builtin_amdgcn_sched_barrier(0);
 }
 
 // Clamped loads only where the span leaves the block (workgroup-uniform).
@@ -294,7 +307,7 @@ __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long 
   // merges the edge and interior paths conservatively and then drains the
   // whole vector-memory queue (vmcnt(0)) at the start of every tile's scan
   // -- including the next tiles' prefetch, which defeats the pipelining.
-  __builtin_amdgcn_s_waitcnt(0);
+  if (SDR_EDGE_DRAIN) __builtin_amdgcn_s_waitcnt(0);
 }
 
 template <int D, int T, int R, bool DEMOD, int NW, int NCH>

@@ -34,7 +34,6 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "fir_parts.hpp"
 #include "sdr_common.hpp"
 
 #pragma clang fp contract(off)
@@ -42,10 +41,248 @@
 namespace sdr {
 namespace {
 
+template <int D, int T, int R, bool DEMOD, int NW>
+struct Geom {
+  static constexpr int NTH = 64 * NW;                               // threads per workgroup
+  static_assert((D * R) % 4 == 0, "lane windows must start on 16-B boundaries");
+  static constexpr int E = DEMOD ? R : 0;                          // overlap outputs per wave
+  static constexpr int WADV = 64 * R - E;                          // new outputs per wave
+  static constexpr int ADV = NW * WADV;                            // new outputs per tile
+  static constexpr int HALO = (T - 1 + 3) / 4 * 4;                 // (T-1) rounded up to a float4
+  static constexpr int SPAN = HALO + D * (R - 1) + 1;              // positions one lane reads
+  static constexpr int NCHUNK = (SPAN + 3) / 4;                    // float4 chunks per lane window
+  static constexpr int SPAN4 = 4 * NCHUNK;                         // tap row length
+  // tap-row reuse: rows GR apart are offset by D*GR taps = SH whole chunks
+  static constexpr int GQ = (D % 4 == 0) ? 1 : (D % 2 == 0) ? 2 : 4;
+  static constexpr int GR = GQ < R ? GQ : R;                       // tap rows read from LDS per chunk
+  static constexpr int SH = D * GR / 4;                            // chunk shift between reused rows
+  static constexpr int LDS_LEN = D * ((NW - 1) * WADV + 63 * R) + SPAN4;  // floats per channel
+  static constexpr int LDS4 = LDS_LEN / 4;
+  static constexpr int FULL = LDS4 / NTH, REM = LDS4 % NTH;        // staging rows per thread
+  // the block's last STRIP inputs per channel, staged by tile 0: the
+  // prev_* recompute (D+T-1 inputs) and the new state (ns <= STRIP)
+  static constexpr int STRIP = ((D + T - 1 > 128 ? D + T - 1 : 128) + 3) / 4 * 4;
+  // LDS floats: channels, tap rows, two tail strips
+  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4 + 2 * STRIP;
+};
+
+__device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp) {
+  // src/filter.cpp:88-98
+  const float env = (float)((double)I * (double)I + (double)Q * (double)Q);
+  if (env == 0.0f) return 0.0f;
+  const float a = I * (Q - qp);
+  const float b = Q * (I - ip);
+  return (a - b) / env;
+}
+
+// Input sample p (>= 0) of channel c of one stream.
+template <Src SRC>
+__device__ __forceinline__ float in_at(const float* x, const uint8_t* iq, int c, long long p) {
+  if constexpr (SRC == Src::F32) {
+    return x[p];
+  } else {
+    return u8_to_f32(iq[2 * p + c]);
+  }
+}
+
+// Element of the tile span at position p: x~[p], zero outside [-ns, n).
+// A guarded load (exec-masked), no branches around it.
+template <Src SRC>
+__device__ __forceinline__ float edge_at(const float* x, const uint8_t* iq, int c, const float* st, int ns,
+                                         long long n, long long p) {
+  const bool in_state = p < 0;
+  const bool valid = p >= -ns && p < n;
+  float v = 0.0f;
+  if constexpr (SRC == Src::F32) {
+    const float* src = in_state ? st + (ns + p) : x + p;
+    if (valid) v = *src;
+  } else {
+    if (valid) v = in_state ? st[ns + p] : u8_to_f32(iq[2 * p + c]);
+  }
+  return v;
+}
+
+// Where one tile lives.
+struct TileRef {
+  int s;              // stream
+  int t;              // tile within the stream
+  long long m_start;  // first output the tile computes (includes the wave overlap)
+  long long pb;       // stream position of LDS index 0
+  const float* x0;
+  const float* x1;
+  const uint8_t* iq;
+  float* st0;
+  float* st1;
+};
+
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ __forceinline__ TileRef tile_ref(const FirLaunch& a, int lin) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  TileRef r;
+  r.s = lin / a.tiles_per_stream;
+  r.t = lin - r.s * a.tiles_per_stream;
+  r.m_start = (long long)r.t * G::ADV - G::E;
+  r.pb = (long long)D * r.m_start - G::HALO;
+  r.st0 = a.state0 + (long long)r.s * a.ns;
+  r.st1 = NCH == 2 ? a.state1 + (long long)r.s * a.ns : nullptr;
+  r.x0 = r.x1 = nullptr;
+  r.iq = nullptr;
+  if constexpr (SRC == Src::F32) {
+    r.x0 = a.x0 + (long long)r.s * a.x_stride;
+    if (NCH == 2) r.x1 = a.x1 + (long long)r.s * a.x_stride;
+  } else {
+    r.iq = a.iq + (long long)r.s * a.x_stride;
+  }
+  return r;
+}
+
+// A tile no clamped chunk of which holds a sample a stored output reads:
+// its span starts at p >= 0 and, when n is not a multiple of 4, ends before
+// the chunk straddling n.  (Chunks past n only feed outputs >= n/D, which
+// are never stored.)
+template <int D, int T, int R, bool DEMOD, int NW>
+__device__ __forceinline__ bool interior(const TileRef& tr, long long n) {
+  const long long n4 = n & ~3LL;
+  return tr.pb >= 0 && (n4 == n || tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n4);
+}
+
+// Issue every global load of one tile span into registers (16-B f32 / 8-B
+// u8 coalesced vectors).  Chunk addresses are clamped into the block, so an
+// edge tile loads in-bounds but partly wrong data that edge_fill() then
+// overwrites.  No wait: stage_store consumes the registers.
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC, bool CLAMP>
+__device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, int tid,
+                                           float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                           float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  auto load4 = [&](int i, float4& a0, float4& a1) {
+    long long p = tr.pb + 4LL * i;
+    if constexpr (CLAMP) {
+      const long long pmax = (n & ~3LL) - 4;  // last whole aligned chunk
+      p = p < 0 ? 0 : (p > pmax ? pmax : p);
+    }
+    if constexpr (SRC == Src::F32) {
+      a0 = *reinterpret_cast<const float4*>(tr.x0 + p);
+      if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
+    } else {
+      const uint2 b = *reinterpret_cast<const uint2*>(tr.iq + 2 * p);
+      a0 = make_float4(u8_byte_to_f32<0>(b.x), u8_byte_to_f32<2>(b.x), u8_byte_to_f32<0>(b.y),
+                       u8_byte_to_f32<2>(b.y));
+      a1 = make_float4(u8_byte_to_f32<1>(b.x), u8_byte_to_f32<3>(b.x), u8_byte_to_f32<1>(b.y),
+                       u8_byte_to_f32<3>(b.y));
+    }
+  };
+#pragma unroll
+  for (int it = 0; it < G::FULL; ++it) load4(tid + it * G::NTH, v0[it], v1[it]);
+  // ragged last row: clamp the index (a redundant load) so every register
+  // is defined and the arrays stay in VGPRs
+  if (G::REM) load4(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL]);
+}
+
+// Clamped loads only where the span leaves the block (workgroup-uniform).
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int tid,
+                                           float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                           float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  if (tr.pb >= 0 && tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n)
+    stage_load_impl<D, T, R, DEMOD, NW, NCH, SRC, false>(tr, n, tid, v0, v1);
+  else
+    stage_load_impl<D, T, R, DEMOD, NW, NCH, SRC, true>(tr, n, tid, v0, v1);
+}
+
+// Edge tiles (a stream's first tile, and the one holding the chunk that
+// straddles n when n % 4 != 0): after the clamped vector fill, rewrite the
+// span elements a stored output reads whose chunk was clamped -- the old
+// state before the block, [pb, 0), and the true samples of the straddling
+// chunk, [n & ~3, n).  With `strip`, also stage the block's last STRIP
+// inputs (old state where p < 0) for tile 0's state carry.  The loads are
+// issued in batches of four per thread before any LDS write, so an edge tile
+// costs about one memory latency, not one per element.
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+__device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long n, int ns, float* lds0, float* lds1,
+                                          bool strip, float* strip0, float* strip1) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  const long long n4 = n & ~3LL;
+  const int lo_end = tr.pb < 0 ? (int)(-tr.pb < G::LDS_LEN ? -tr.pb : G::LDS_LEN) : 0;
+  auto clampi = [](long long v, int lo, int hi) { return (int)(v < lo ? lo : (v > hi ? hi : v)); };
+  const int hi_beg = clampi(n4 - tr.pb, lo_end, G::LDS_LEN);
+  const int hi_end = clampi(n - tr.pb, hi_beg, G::LDS_LEN);
+  const int nfix = lo_end + (hi_end - hi_beg);
+  const int ntot = nfix + (strip ? G::STRIP : 0);
+  for (int e0 = 0; e0 < ntot; e0 += 4 * G::NTH) {
+    float v0[4], v1[4];
+    float* d0[4];
+    float* d1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * G::NTH + tid;
+      long long p;
+      if (e < lo_end) {
+        p = tr.pb + e;
+        d0[u] = lds0 + e;
+        d1[u] = lds1 + e;
+      } else if (e < nfix) {
+        const int i = hi_beg + (e - lo_end);
+        p = tr.pb + i;
+        d0[u] = lds0 + i;
+        d1[u] = lds1 + i;
+      } else {
+        const int j = e - nfix;
+        p = n - G::STRIP + j;
+        d0[u] = strip0 + j;
+        d1[u] = strip1 + j;
+      }
+      v0[u] = 0.0f;
+      v1[u] = 0.0f;
+      if (e < ntot) {
+        v0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+        if (NCH == 2) v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * G::NTH + tid < ntot) {
+        *d0[u] = v0[u];
+        if (NCH == 2) *d1[u] = v1[u];
+      }
+    }
+  }
+}
+
+template <int D, int T, int R, bool DEMOD, int NW, int NCH>
+__device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
+                                            const float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                            const float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+#pragma unroll
+  for (int it = 0; it < G::FULL; ++it) {
+    const int i = tid + it * G::NTH;
+    *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[it];
+    if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[it];
+  }
+  if (G::REM && tid < G::REM) {
+    const int i = tid + G::FULL * G::NTH;
+    *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[G::FULL];
+    if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[G::FULL];
+  }
+}
+
+// f(integral_constant<int, B>), f(<B+1>), ..., f(<E-1>): a fully unrolled
+// loop whose index is a constant expression in the body.
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 // TM = where the taps live: 0 LDS broadcast rows, 1 SGPRs (NPASS passes).
 // PF = prefetch depth: tile i+PF's loads are issued (into one of PF
 // register sets) before tile i is computed.
-// FMA: fused multiply-add FIR arithmetic (SDR_ARITH_FMA, SGPR-tap scan only).
+// FMA = the fused multiply-add arithmetic mode (SDR_ARITH_FMA, SGPR taps
+// only): same taps, same order, one rounding per tap instead of two -- not
+// the reference's bits, within the fp32 tolerance of DESIGN.md 2.
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, int PF, bool FMA = false>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
   static_assert(PF == 1 || PF == 2, "prefetch depth");
@@ -102,23 +339,24 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   Stage sa0, sa1, sb0, sb1;
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = sb0[i] = sb1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  // Every tile issues the same loads on every path: a prefetch past the
-  // workgroup's last tile reloads that tile (L2 hits), and ablate 1 (timing
-  // only) keeps reloading the first one.  Conditional prefetches make
-  // hipcc's waitcnt pass merge unequal vmcnt histories and drain the queue
-  // (vmcnt(0)) before every staging store, i.e. no prefetch at all.
-  auto pf_tile = [&](int lin) { return a.ablate == 1 ? first : (lin < last ? lin : last - 1); };
-  stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, pf_tile(first)), n, tid, sa0, sa1);
-  if constexpr (PF == 2)
-    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, pf_tile(first + step)), n, tid,
-                                             sb0, sb1);
+  if (a.ablate != 1) {
+    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
+    if (PF == 2 && first + step < last)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first + step), n, tid, sb0,
+                                               sb1);
+  }
 
   auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
     // Old prev_I/prev_Q, read before this workgroup rewrites them at the
     // end of the iteration (tile 0 only).
     float old_pi = 0.0f, old_pq = 0.0f;
-    if constexpr (DEMOD) load_prev(a, tr, old_pi, old_pq);
+    if constexpr (DEMOD) {
+      if (tr.t == 0 && tid == 1) {
+        old_pi = a.prev0[tr.s];
+        old_pq = a.prev1[tr.s];
+      }
+    }
 
     // ---- 1. registers -> LDS (after every read of the previous tile), then
     // prefetch the next tile into the registers just freed.  Tile 0 also
@@ -126,17 +364,15 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
     // rewrites the state below.
     __syncthreads();
-    // f32 loads are untracked (ldg4_async): wait for this set, leaving the
-    // PF-1 sets issued after it in flight
-    if constexpr (SRC == Src::F32) vm_wait<(PF - 1) * NCH * G::STAGE_LOADS>(v0, v1);
     stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
     if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
       edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, tr.t == 0, strip0, strip1);
     }
     __syncthreads();
-    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, pf_tile(lin + PF * step)), n,
-                                             tid, v0, v1);
+    if (lin + PF * step < last && a.ablate != 1)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF * step), n, tid, v0,
+                                               v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
@@ -208,35 +444,165 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
-        scan_sgpr<D, T, R, NCH, G, FMA>(w0, w1, h, acc0, acc1, a.ablate);
+        // Taps as SGPR operands of the multiplies: no LDS tap traffic.  All
+        // T taps do not fit the SGPR file beside the addressing, so the
+        // window is walked in NPASS passes over consecutive tap ranges
+        // [k0, k1), each loading its taps once (scalar loads from the
+        // constant address space, one wait) -- every output still visits
+        // k = 0..T-1 in order, the passes only split its chain.
+        constexpr int NPASS = 3, KP = (T + NPASS - 1) / NPASS;
+        using hconst = const __attribute__((address_space(4))) float*;
+        const hconst hc = (hconst)h;
+        float hs[KP];
+        static_for<0, NPASS>([&](auto pi) {
+          constexpr int k0 = decltype(pi)::value * KP;
+          constexpr int k1 = k0 + KP < T ? k0 + KP : T;
+          // ablate 4 (timing only): one pass of three -- how much a cheaper scan buys
+          if (a.ablate == 4 && k0 > 0) return;
+#pragma unroll
+          for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
+#pragma unroll
+          for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
+          // window positions w = HALO + D r - k this pass touches
+          constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
+          constexpr int whi = G::HALO + D * (R - 1) - k0;
+          constexpr int clo = wlo / 4, chi = whi / 4;
+          float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * chi);
+          float4 q1 = q0;
+          if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * chi);
+          static_for<0, chi - clo + 1>([&](auto ci) {
+            constexpr int c = chi - decltype(ci)::value;
+            float4 n0 = q0, n1 = q1;
+            if constexpr (c > clo) {
+              n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
+              if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+            }
+            const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+            const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+            static_for<0, 4>([&](auto ji) {
+              constexpr int j = 3 - decltype(ji)::value;
+              static_for<0, R>([&](auto ri) {
+                constexpr int r = decltype(ri)::value;
+                constexpr int k = G::HALO + D * r - (4 * c + j);
+                if constexpr (k >= k0 && k < k1) {
+                  if constexpr (FMA) {
+                    acc0[r] = __builtin_fmaf(hs[k - k0], e0[j], acc0[r]);
+                    if (NCH == 2) acc1[r] = __builtin_fmaf(hs[k - k0], e1[j], acc1[r]);
+                  } else {
+                    acc0[r] = acc0[r] + hs[k - k0] * e0[j];
+                    if (NCH == 2) acc1[r] = acc1[r] + hs[k - k0] * e1[j];
+                  }
+                }
+              });
+            });
+            q0 = n0;
+            q1 = n1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
+            __builtin_amdgcn_sched_barrier(0);
+          });
+        });
       }
     }
 
-    tile_epilogue<D, T, R, NW, NCH, DEMOD, SRC, FMA>(a, tr, h, tid, lane, wave, n, nout, ns, acc0, acc1, old_pi, old_pq,
-                                               strip0, strip1);
+    const long long m0 = tr.m_start + (long long)wave * G::WADV + (long long)R * lane;  // this lane's first output
+    if constexpr (DEMOD) {
+      // ---- 3. discriminator in registers.  The decimated sample before
+      // output r=0 is lane-1's last output (a wave shuffle); lane 0's
+      // outputs are the wave's overlap and are not stored; at the start of
+      // the stream (tile 0, wave 0, lane 1 -> output 0) it is the carried prev_*.
+      float pI = __shfl_up(acc0[R - 1], 1, 64);
+      float pQ = __shfl_up(acc1[R - 1], 1, 64);
+      if (tr.t == 0 && tid == 1) {
+        pI = old_pi;
+        pQ = old_pq;
+      }
+      float d[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float ip = r ? acc0[r - 1] : pI;
+        const float qp = r ? acc1[r - 1] : pQ;
+        d[r] = demod_one(acc0[r], acc1[r], ip, qp);
+      }
+      float* o = a.out + (long long)tr.s * a.out_stride;
+      // vector stores when the row keeps R-float groups aligned (uniform)
+      const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+      // ablate 3 (timing only): no output stores unless the result is a
+      // value it never is, so the scan still runs
+      if (lane >= 1 && (a.ablate != 3 || d[0] == 12345.0f)) {
+        if (vec && m0 + R <= nout) {
+          if constexpr (R == 2) {
+            *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);
+          } else if constexpr (R == 4) {
+            *reinterpret_cast<float4*>(o + m0) = make_float4(d[0], d[1], d[2], d[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (m0 + r < nout) o[m0 + r] = d[r];
+        }
+      }
+    } else {
+      float* o = a.y0 + (long long)tr.s * a.y_stride;
+      const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+      if (vec && m0 + R <= nout) {
+        if constexpr (R == 4) {
+          *reinterpret_cast<float4*>(o + m0) = make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
+        } else if constexpr (R == 2) {
+          *reinterpret_cast<float2*>(o + m0) = make_float2(acc0[0], acc0[1]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) o[m0 + r] = acc0[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (m0 + r < nout) o[m0 + r] = acc0[r];
+      }
+    }
+
+    // ---- 4. state carry (tile 0 only; every read of the old values
+    // happened before the barriers above)
+    if (tr.t == 0) {
+      if constexpr (DEMOD) {
+        // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
+        // recomputed in the reference's order from the staged strip:
+        // input D*(nout-1) - k = n - D - k sits at strip index STRIP - D - k
+        if (tid == 0) {
+          float yi = 0.0f, yq = 0.0f;
+          for (int k = 0; k < T; ++k) {
+            const float hk = h[k];
+            yi = yi + hk * strip0[G::STRIP - D - k];
+            yq = yq + hk * strip1[G::STRIP - D - k];
+          }
+          a.prev0[tr.s] = yi;
+          a.prev1[tr.s] = yq;
+        }
+      }
+      // state <- last ns input samples (src/filter.cpp:139)
+      if (ns <= G::STRIP) {
+        for (int j = tid; j < ns; j += NTH) {
+          tr.st0[j] = strip0[G::STRIP - ns + j];
+          if (NCH == 2) tr.st1[j] = strip1[G::STRIP - ns + j];
+        }
+      } else {
+        for (int j = tid; j < ns; j += NTH) {
+          const long long p = n - ns + j;
+          tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, p);
+          if (NCH == 2) tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
+        }
+      }
+    }
   };
 
-  if constexpr (PF == 2) {
-    // Both tiles of a pair run unconditionally inside the loop, the odd
-    // trailing tile after it.  A conditional second tile would give hipcc's
-    // waitcnt pass a path back to the loop head on which the other register
-    // set's loads were not issued; merging it makes every stage_store wait
-    // vmcnt(0) -- draining the prefetch behind it, i.e. no pipelining.
-    int lin = first;
-    for (; lin + step < last; lin += 2 * step) {
-      tile(lin, sa0, sa1);
-      tile(lin + step, sb0, sb1);
+  for (int lin = first; lin < last; lin += PF * step) {
+    tile(lin, sa0, sa1);
+    if constexpr (PF == 2) {
+      if (lin + step < last) tile(lin + step, sb0, sb1);
     }
-    if (lin < last) tile(lin, sa0, sa1);
-  } else {
-    for (int lin = first; lin < last; lin += step) tile(lin, sa0, sa1);
-  }
-  // The last prefetches are never consumed.  Their values must stay live
-  // until they have landed: an untracked load (ldg4_async) whose value the
-  // compiler believes dead may land in registers it has already reused.
-  if constexpr (SRC == Src::F32) {
-    vm_wait<0>(sa0, sa1);
-    if constexpr (PF == 2) vm_wait<0>(sb0, sb1);
   }
 }
 
@@ -357,8 +723,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
   }();
   a.ablate = ablate;
   const size_t lds = (size_t)(G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float);  // TM 1: no tap rows
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, PF, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a,
-                     h);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, PF, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();
 }
 
