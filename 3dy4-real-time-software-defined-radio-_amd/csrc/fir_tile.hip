@@ -38,6 +38,16 @@
 
 #pragma clang fp contract(off)
 
+// Build switches (same-box A/B with scripts/build_ab_tree.sh):
+// SDR_EDGE_DRAIN: retire edge-tile loads inside the edge path;
+// SDR_PREV_SCALAR: read the carried prev_I/prev_Q with scalar loads.
+#ifndef SDR_EDGE_DRAIN
+#define SDR_EDGE_DRAIN 1
+#endif
+#ifndef SDR_PREV_SCALAR
+#define SDR_PREV_SCALAR 1
+#endif
+
 namespace sdr {
 namespace {
 
@@ -247,6 +257,13 @@ __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long 
       }
     }
   }
+#if SDR_EDGE_DRAIN
+  // Retire the edge loads inside the (rare) edge path.  Left pending, they
+  // make hipcc's waitcnt pass merge the edge and interior paths
+  // conservatively and drain the whole vector-memory queue (vmcnt(0)) at
+  // every tile's scan -- the next tiles' prefetch included.
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
 }
 
 template <int D, int T, int R, bool DEMOD, int NW, int NCH>
@@ -352,10 +369,23 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // end of the iteration (tile 0 only).
     float old_pi = 0.0f, old_pq = 0.0f;
     if constexpr (DEMOD) {
+#if SDR_PREV_SCALAR
+      // scalar loads (lgkmcnt, not vmcnt): a conditional vector load here
+      // makes the waitcnt pass drain the prefetch queue at the scan.  The
+      // value is the launch's input: only this workgroup rewrites it, after
+      // this read.
+      if (tr.t == 0) {  // workgroup-uniform
+        using cf = const __attribute__((address_space(4))) float*;
+        const int s = __builtin_amdgcn_readfirstlane(tr.s);
+        old_pi = ((cf)a.prev0)[s];
+        old_pq = ((cf)a.prev1)[s];
+      }
+#else
       if (tr.t == 0 && tid == 1) {
         old_pi = a.prev0[tr.s];
         old_pq = a.prev1[tr.s];
       }
+#endif
     }
 
     // ---- 1. registers -> LDS (after every read of the previous tile), then
