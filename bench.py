@@ -67,11 +67,13 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--warm-seconds", type=float, default=0.25,
+                    help="after the W warmup steps, keep running untimed steps for this long (clock ramp)")
     ap.add_argument("--no-fma-variant", action="store_true", help="skip the SDR_ARITH_FMA side measurement")
     ap.add_argument("--arith", choices=("exact", "fma"), default=os.environ.get("SDR_BENCH_ARITH", "exact"),
                     help="front-end FIR arithmetic: the reference's bits (exact) or one fused multiply-add per tap "
@@ -308,9 +310,18 @@ def main():
         tolerance = {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale,
                      "norm": "sum|h| * max|x|", "rms_err": float((got - ref).pow(2).mean().sqrt())}
 
+    # W warmup steps, then more of the same launches until >= --warm-seconds
+    # of wall time has passed: an idle MI355X sits at ~0.1 GHz and its clock
+    # ramps over tens of ms; a few warmup steps (<1 ms) would time part of
+    # the ramp, not the sustained rate a streaming receiver runs at.
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < args.warm_seconds:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -366,6 +377,12 @@ def main():
         ctx.set_arith(sdrhip.ARITH_FMA)
         for _ in range(max(args.warmup, 2)):
             step()
+        torch.cuda.synchronize(dev)
+        t_warm = time.perf_counter()
+        while time.perf_counter() - t_warm < args.warm_seconds:
+            for _ in range(10):
+                step()
+            torch.cuda.synchronize(dev)
         f0 = torch.cuda.Event(enable_timing=True)
         f1 = torch.cuda.Event(enable_timing=True)
         f0.record(stream)
