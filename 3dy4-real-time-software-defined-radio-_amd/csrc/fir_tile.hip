@@ -775,14 +775,17 @@ Variant variant_for(int D, bool demod, Src src) {
     const int got = std::sscanf(env, "%dx%d%c", &r, &w, &m);
     if (got >= 2) {
       const Variant v{r, w, m == 'r' || m == 'p' ? 1 : 0, m == 'p' ? 2 : 1, m == 'p' ? 24 : 32};
-      const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
+      const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 2 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
                          (D == 5 && r == 4 && (w == 1 || w == 4)) ||
                          (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
       if (known) return v;
     }
   }
   switch (D) {
-    case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 2, 24} : Variant{2, 1, 1, 1, 32};
+    // f32 fused: prefetch depth 1 (≈115 VGPRs, 4 waves/SIMD) and 64 one-wave
+    // workgroups per CU beat depth 2 (165 VGPRs, 3 waves/SIMD) by 4-6 % once
+    // the clock has ramped (same-box A/B)
+    case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 1, 64} : Variant{2, 1, 1, 1, 32};
     case 5: return {4, 1, 1, 1, 32};
     case 1: return {4, 1, 0, 1, 32};
     default: return {0, 0, 0, 1, 32};
@@ -828,6 +831,8 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
     if (v.tm == 1) {
       switch (key) {
         case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 100202: return run_tile<10, 101, 2, 2, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         default: break;
