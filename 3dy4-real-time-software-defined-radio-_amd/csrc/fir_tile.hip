@@ -73,7 +73,10 @@ struct Geom {
   // prev_* recompute (D+T-1 inputs) and the new state (ns <= STRIP)
   static constexpr int STRIP = ((D + T - 1 > 128 ? D + T - 1 : 128) + 3) / 4 * 4;
   // LDS floats: channels, tap rows, two tail strips
-  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4 + 2 * STRIP;
+  // (the strips reuse the channel buffers after tile 0's scan: LDS per
+  // wave sets the occupancy, 13 -> 14 one-wave workgroups per CU at D = 10)
+  static_assert(STRIP <= LDS_LEN, "strip staged into the channel buffers");
+  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4;
 };
 
 __device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp) {
@@ -176,10 +179,12 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
       if (NCH == 2) a1 = *reinterpret_cast<const float4*>(tr.x1 + p);
     } else {
       const uint2 b = *reinterpret_cast<const uint2*>(tr.iq + 2 * p);
-      a0 = make_float4(u8_byte_to_f32<0>(b.x), u8_byte_to_f32<2>(b.x), u8_byte_to_f32<0>(b.y),
-                       u8_byte_to_f32<2>(b.y));
-      a1 = make_float4(u8_byte_to_f32<1>(b.x), u8_byte_to_f32<3>(b.x), u8_byte_to_f32<1>(b.y),
-                       u8_byte_to_f32<3>(b.y));
+      // the raw wire bytes stay in the prefetch registers (2 VGPRs per
+      // chunk); stage_store unpacks them.  Unpacking here would consume the
+      // load right after issuing it -- an immediate vmcnt wait, i.e. no
+      // prefetch at all.
+      a0.x = __uint_as_float(b.x);
+      a0.y = __uint_as_float(b.y);
     }
   };
 #pragma unroll
@@ -266,22 +271,27 @@ __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long 
 #endif
 }
 
-template <int D, int T, int R, bool DEMOD, int NW, int NCH>
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
 __device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
                                             const float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
                                             const float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   using G = Geom<D, T, R, DEMOD, NW>;
+  // u8: v0[i].x/.y hold 8 raw interleaved wire bytes (I0 Q0 I1 Q1 | I2 Q2 I3 Q3)
+  auto put = [&](int i, const float4& a0, const float4& a1) {
+    if constexpr (SRC == Src::U8) {
+      const uint32_t bx = __float_as_uint(a0.x), by = __float_as_uint(a0.y);
+      *reinterpret_cast<float4*>(lds0 + 4 * i) = make_float4(u8_byte_to_f32<0>(bx), u8_byte_to_f32<2>(bx),
+                                                             u8_byte_to_f32<0>(by), u8_byte_to_f32<2>(by));
+      *reinterpret_cast<float4*>(lds1 + 4 * i) = make_float4(u8_byte_to_f32<1>(bx), u8_byte_to_f32<3>(bx),
+                                                             u8_byte_to_f32<1>(by), u8_byte_to_f32<3>(by));
+    } else {
+      *reinterpret_cast<float4*>(lds0 + 4 * i) = a0;
+      if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = a1;
+    }
+  };
 #pragma unroll
-  for (int it = 0; it < G::FULL; ++it) {
-    const int i = tid + it * G::NTH;
-    *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[it];
-    if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[it];
-  }
-  if (G::REM && tid < G::REM) {
-    const int i = tid + G::FULL * G::NTH;
-    *reinterpret_cast<float4*>(lds0 + 4 * i) = v0[G::FULL];
-    if (NCH == 2) *reinterpret_cast<float4*>(lds1 + 4 * i) = v1[G::FULL];
-  }
+  for (int it = 0; it < G::FULL; ++it) put(tid + it * G::NTH, v0[it], v1[it]);
+  if (G::REM && tid < G::REM) put(tid + G::FULL * G::NTH, v0[G::FULL], v1[G::FULL]);
 }
 
 // f(integral_constant<int, B>), f(<B+1>), ..., f(<E-1>): a fully unrolled
@@ -312,8 +322,8 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   float* lds0 = smem;
   float* lds1 = smem + G::LDS_LEN;
   float* htab = smem + 2 * G::LDS_LEN;                 // R tap rows (TM 0)
-  float* strip0 = htab + (TM == 0 ? R * G::SPAN4 : 0);  // the block's last inputs (tile 0)
-  float* strip1 = strip0 + G::STRIP;
+  float* strip0 = lds0;  // the block's last inputs (tile 0, after its scan)
+  float* strip1 = lds1;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -394,10 +404,10 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
     // rewrites the state below.
     __syncthreads();
-    stage_store<D, T, R, DEMOD, NW, NCH>(lds0, lds1, tid, v0, v1);
+    stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
     if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
-      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, tr.t == 0, strip0, strip1);
+      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, false, strip0, strip1);
     }
     __syncthreads();
     if (lin + PF * step < last && a.ablate != 1)
@@ -597,6 +607,35 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // ---- 4. state carry (tile 0 only; every read of the old values
     // happened before the barriers above)
     if (tr.t == 0) {
+      // stage the block's last STRIP inputs (old state where p < 0: the
+      // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) into the
+      // channel buffers, free once every lane's scan has read them
+      __syncthreads();
+      for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
+        float v0[4], v1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * NTH + tid;
+          const long long p = n - G::STRIP + j;
+          v0[u] = v1[u] = 0.0f;
+          if (j < G::STRIP) {
+            v0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+            if (NCH == 2) v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * NTH + tid;
+          if (j < G::STRIP) {
+            strip0[j] = v0[u];
+            if (NCH == 2) strip1[j] = v1[u];
+          }
+        }
+      }
+#if SDR_EDGE_DRAIN
+      __builtin_amdgcn_s_waitcnt(0);  // as in edge_fill: keep the waitcnt pass from draining at the next scan
+#endif
+      __syncthreads();
       if constexpr (DEMOD) {
         // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
         // recomputed in the reference's order from the staged strip:
