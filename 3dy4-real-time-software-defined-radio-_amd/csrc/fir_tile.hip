@@ -247,7 +247,7 @@ __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int t
 // costs about one memory latency, not one per element.
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
 __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long n, int ns, float* lds0, float* lds1,
-                                          bool strip, float* strip0, float* strip1) {
+                                          bool strip, float* strip0, float* strip1, int c0 = 0) {
   using G = Geom<D, T, R, DEMOD, NW>;
   const long long n4 = n & ~3LL;
   const int lo_end = tr.pb < 0 ? (int)(-tr.pb < G::LDS_LEN ? -tr.pb : G::LDS_LEN) : 0;
@@ -282,7 +282,7 @@ __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long 
       v0[u] = 0.0f;
       v1[u] = 0.0f;
       if (e < ntot) {
-        v0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+        v0[u] = edge_at<SRC>(tr.x0, tr.iq, c0, tr.st0, ns, n, p);
         if (NCH == 2) v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
       }
     }
@@ -326,6 +326,26 @@ __device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
   if (G::REM && tid < G::REM) put(tid + G::FULL * G::NTH, v0[G::FULL], v1[G::FULL]);
 }
 
+// Split mode, u8 wire: store channel 0 (bytes 0, 2 of each raw word) to
+// `buf` and unpack channel 1 (bytes 1, 3) into v1 as floats, which frees v0
+// for the next tile's raw prefetch before channel 0 is scanned.
+template <int D, int T, int R, bool DEMOD, int NW>
+__device__ __forceinline__ void stage_u8_split(float* buf, int tid,
+                                               const float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                               float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+#pragma unroll
+  for (int it = 0; it <= G::FULL; ++it) {
+    if (it == G::FULL && !G::REM) break;
+    const uint32_t bx = __float_as_uint(v0[it].x), by = __float_as_uint(v0[it].y);
+    const int i = tid + it * G::NTH;
+    if (it < G::FULL || tid < G::REM)
+      *reinterpret_cast<float4*>(buf + 4 * i) = make_float4(u8_byte_to_f32<0>(bx), u8_byte_to_f32<2>(bx),
+                                                            u8_byte_to_f32<0>(by), u8_byte_to_f32<2>(by));
+    v1[it] = make_float4(u8_byte_to_f32<1>(bx), u8_byte_to_f32<3>(bx), u8_byte_to_f32<1>(by), u8_byte_to_f32<3>(by));
+  }
+}
+
 // f(integral_constant<int, B>), f(<B+1>), ..., f(<E-1>): a fully unrolled
 // loop whose index is a constant expression in the body.
 template <int B, int E, class F>
@@ -342,7 +362,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 // FMA = the fused multiply-add arithmetic mode (SDR_ARITH_FMA, SGPR taps
 // only): same taps, same order, one rounding per tap instead of two -- not
 // the reference's bits, within the fp32 tolerance of DESIGN.md 2.
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, int PF, bool FMA = false>
+// SPLIT = one LDS buffer: channel 0 is staged and scanned, then channel 1
+// (NCH == 2, SGPR taps, prefetch depth 1).  Half the LDS per wave, so the
+// VGPRs, not the LDS, set the occupancy (14 -> 16 waves per CU at D = 10).
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, int PF, bool FMA = false,
+          bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
   static_assert(PF == 1 || PF == 2, "prefetch depth");
   using G = Geom<D, T, R, DEMOD, NW>;
@@ -352,10 +376,12 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lds0 = smem;
-  float* lds1 = smem + G::LDS_LEN;
+  static_assert(!SPLIT || (NCH == 2 && TM == 1 && PF == 1), "split mode: 2 channels, SGPR taps, prefetch 1");
+  static_assert(!SPLIT || 2 * G::STRIP <= G::LDS_LEN, "split mode: both strips in the one buffer");
+  float* lds1 = SPLIT ? smem : smem + G::LDS_LEN;
   float* htab = smem + 2 * G::LDS_LEN;                 // R tap rows (TM 0)
   float* strip0 = lds0;  // the block's last inputs (tile 0, after its scan)
-  float* strip1 = lds1;
+  float* strip1 = SPLIT ? smem + G::STRIP : lds1;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -435,16 +461,18 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // stages the block's last STRIP inputs (old state where p < 0: the
     // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
     // rewrites the state below.
-    __syncthreads();
-    stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
-    if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
+    if constexpr (!SPLIT) {
       __syncthreads();
-      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, false, strip0, strip1);
+      stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
+      if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
+        __syncthreads();
+        edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, false, strip0, strip1);
+      }
+      __syncthreads();
+      if (lin + PF * step < last && a.ablate != 1)
+        stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF * step), n, tid,
+                                                 v0, v1);
     }
-    __syncthreads();
-    if (lin + PF * step < last && a.ablate != 1)
-      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF * step), n, tid, v0,
-                                               v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
@@ -464,7 +492,95 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       acc0[r] = 0.0f;
       acc1[r] = 0.0f;
     }
-    if (a.ablate == 2) {
+    if constexpr (SPLIT) {
+      // One channel at a time through the single buffer lds0 (== lds1):
+      //   store ch0 -> [edge ch0] -> prefetch next ch0 -> scan ch0 ->
+      //   store ch1 -> [edge ch1] -> prefetch next ch1 -> scan ch1.
+      // u8: the raw words carry both channels; ch1 is unpacked into v1 at
+      // the ch0 store, so the next tile's raw prefetch can go into v0 then.
+      const bool edge = tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n);  // workgroup-uniform
+      const bool more = lin + step < last && a.ablate != 1;
+      const TileRef tn = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, more ? lin + step : lin);
+      TileRef tq = tr;  // channel 1 seen as channel 0
+      tq.x0 = tr.x1;
+      tq.st0 = tr.st1;
+      // single-channel scan, SGPR taps in NPASS passes (as below)
+      auto scan1 = [&](const float* w, float (&acc)[R]) __attribute__((always_inline)) {
+        constexpr int NPASS = 3, KP = (T + NPASS - 1) / NPASS;
+        using hconst = const __attribute__((address_space(4))) float*;
+        const hconst hc = (hconst)h;
+        float hs[KP];
+        static_for<0, NPASS>([&](auto pi) {
+          constexpr int k0 = decltype(pi)::value * KP;
+          constexpr int k1 = k0 + KP < T ? k0 + KP : T;
+#pragma unroll
+          for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
+#pragma unroll
+          for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
+          constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
+          constexpr int whi = G::HALO + D * (R - 1) - k0;
+          constexpr int clo = wlo / 4, chi = whi / 4;
+          float4 q = *reinterpret_cast<const float4*>(w + 4 * chi);
+          static_for<0, chi - clo + 1>([&](auto ci) {
+            constexpr int c = chi - decltype(ci)::value;
+            float4 nq = q;
+            if constexpr (c > clo) nq = *reinterpret_cast<const float4*>(w + 4 * (c - 1));
+            const float e[4] = {q.x, q.y, q.z, q.w};
+            static_for<0, 4>([&](auto ji) {
+              constexpr int j = 3 - decltype(ji)::value;
+              static_for<0, R>([&](auto ri) {
+                constexpr int r = decltype(ri)::value;
+                constexpr int k = G::HALO + D * r - (4 * c + j);
+                if constexpr (k >= k0 && k < k1) {
+                  if constexpr (FMA)
+                    acc[r] = __builtin_fmaf(hs[k - k0], e[j], acc[r]);
+                  else
+                    acc[r] = acc[r] + hs[k - k0] * e[j];
+                }
+              });
+            });
+            q = nq;
+#pragma unroll
+            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+            __builtin_amdgcn_sched_barrier(0);
+          });
+        });
+      };
+      // ---- channel 0
+      __syncthreads();
+      if constexpr (SRC == Src::U8)
+        stage_u8_split<D, T, R, DEMOD, NW>(lds0, tid, v0, v1);
+      else
+        stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds0, lds0, tid, v0, v0);
+      if (edge) {
+        __syncthreads();
+        edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, tid, n, ns, lds0, lds0, false, strip0, strip1, 0);
+      }
+      __syncthreads();
+      if (more) {
+        if constexpr (SRC == Src::U8)
+          stage_load<D, T, R, DEMOD, NW, 2, SRC>(tn, n, tid, v0, v0);  // raw words of both channels
+        else
+          stage_load<D, T, R, DEMOD, NW, 1, SRC>(tn, n, tid, v0, v0);
+      }
+      scan1(lds0 + lbase, acc0);
+      // ---- channel 1
+      __syncthreads();
+      stage_store<D, T, R, DEMOD, NW, 1, Src::F32>(lds0, lds0, tid, v1, v1);
+      if (edge) {
+        __syncthreads();
+        edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tq, tid, n, ns, lds0, lds0, false, strip0, strip1, 1);
+      }
+      __syncthreads();
+      if constexpr (SRC == Src::F32) {
+        if (more) {
+          TileRef tnq = tn;
+          tnq.x0 = tn.x1;
+          stage_load<D, T, R, DEMOD, NW, 1, SRC>(tnq, n, tid, v1, v1);
+        }
+      }
+      scan1(lds0 + lbase, acc1);
+    } else if (a.ablate == 2) {
       acc0[0] = lds0[lbase];
       acc1[0] = lds1[lbase];
     } else {
@@ -780,7 +896,8 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 // ------------------------------------------------------------ dispatch ----
 // Persistent grid: about `wpc` waves per CU (or the tile count, if smaller),
 // each workgroup walking its share of the tiles (see `walk` in fir_tile).
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM = 0, int PF = 1, bool FMA = false>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM = 0, int PF = 1, bool FMA = false,
+          bool SPLIT = false>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
@@ -823,8 +940,13 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
     return e ? std::atoi(e) : 0;
   }();
   a.ablate = ablate;
-  const size_t lds = (size_t)(G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float);  // TM 1: no tap rows
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, PF, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
+  static const int lds_pad = [] {  // timing experiments only: extra LDS per workgroup (occupancy sweep)
+    const char* e = std::getenv("SDR_LDS_PAD");
+    return e ? std::atoi(e) : 0;
+  }();
+  const size_t lds = (size_t)(SPLIT ? G::LDS_LEN : G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float) +
+                     lds_pad;  // TM 1: no tap rows; SPLIT: one channel buffer
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, PF, FMA, SPLIT>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
   return hipGetLastError();
 }
 
@@ -836,7 +958,10 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
 // SDR_WG_PER_CU override them for experiments.
 struct Variant {
   int R, NW, tm, pf, wpc;  // tm: taps in LDS rows (0) or SGPRs (1); pf: prefetch depth
+  int split = 0;           // fused 2-channel: one LDS buffer, channels in turn (fir_tile SPLIT)
 };
+
+Variant variant_for_default(int D, bool demod, Src src);
 
 Variant variant_for(int D, bool demod, Src src) {
   static const char* env = std::getenv("SDR_FIR_VARIANT");
@@ -845,13 +970,19 @@ Variant variant_for(int D, bool demod, Src src) {
     char m = 0;
     const int got = std::sscanf(env, "%dx%d%c", &r, &w, &m);
     if (got >= 2) {
-      const Variant v{r, w, m == 'r' || m == 'p' ? 1 : 0, m == 'p' ? 2 : 1, m == 'p' ? 24 : 32};
+      // suffix s: SGPR taps, prefetch 1, split channels (fused D = 10 / 5, one wave)
+      const Variant v{r, w, m == 'r' || m == 'p' || m == 's' ? 1 : 0, m == 'p' ? 2 : 1, m == 'p' ? 24 : 32, m == 's'};
+      if (v.split && !(demod && w == 1 && ((D == 10 && r == 2) || (D == 5 && r == 4)))) return variant_for_default(D, demod, src);
       const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 2 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
                          (D == 5 && r == 4 && (w == 1 || w == 4)) ||
                          (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
       if (known) return v;
     }
   }
+  return variant_for_default(D, demod, src);
+}
+
+Variant variant_for_default(int D, bool demod, Src src) {
   switch (D) {
     // f32 fused: prefetch depth 1 (≈115 VGPRs, 4 waves/SIMD) and 64 one-wave
     // workgroups per CU beat depth 2 (165 VGPRs, 3 waves/SIMD) by 4-6 % once
@@ -879,6 +1010,17 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
   const Variant v = variant_for(a.D, DEMOD, SRC);
   const int key = a.D * 10000 + v.R * 100 + v.NW;
   if (a.ntaps == 101) {
+    if constexpr (DEMOD) {
+      if (v.split) {
+        switch (key * 10 + (a.fma ? 1 : 0)) {
+          case 1002010: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 1, false, true>(a, h, st, v.wpc);
+          case 1002011: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 1, true, true>(a, h, st, v.wpc);
+          case 504010: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, 1, false, true>(a, h, st, v.wpc);
+          case 504011: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, 1, true, true>(a, h, st, v.wpc);
+          default: break;
+        }
+      }
+    }
     // SDR_ARITH_FMA: instantiated for the default fused variants (D = 10 and
     // 5); any other shape runs the exact arithmetic (inside the tolerance)
     if constexpr (DEMOD) {
