@@ -53,6 +53,11 @@
 #ifndef SDR_FIR_NT
 #define SDR_FIR_NT 1
 #endif
+// SDR_NPASS: SGPR tap passes of the scan (3: 34 taps per pass fit the SGPR
+// file beside the addressing; fewer passes re-read fewer window chunks).
+#ifndef SDR_NPASS
+#define SDR_NPASS 3
+#endif
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
@@ -506,7 +511,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       tq.st0 = tr.st1;
       // single-channel scan, SGPR taps in NPASS passes (as below)
       auto scan1 = [&](const float* w, float (&acc)[R]) __attribute__((always_inline)) {
-        constexpr int NPASS = 3, KP = (T + NPASS - 1) / NPASS;
+        constexpr int NPASS = SDR_NPASS, KP = (T + NPASS - 1) / NPASS;
         using hconst = const __attribute__((address_space(4))) float*;
         const hconst hc = (hconst)h;
         float hs[KP];
@@ -638,7 +643,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
         // [k0, k1), each loading its taps once (scalar loads from the
         // constant address space, one wait) -- every output still visits
         // k = 0..T-1 in order, the passes only split its chain.
-        constexpr int NPASS = 3, KP = (T + NPASS - 1) / NPASS;
+        constexpr int NPASS = SDR_NPASS, KP = (T + NPASS - 1) / NPASS;
         using hconst = const __attribute__((address_space(4))) float*;
         const hconst hc = (hconst)h;
         float hs[KP];

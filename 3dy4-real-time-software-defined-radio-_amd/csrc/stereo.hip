@@ -46,8 +46,8 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   const float Ki = norm_bw * norm_bw * 3.555f;
   const double step = 2.0 * kPiD * (double)(freq / Fs);  // 2*PI*(freq/Fs), double (PI is a double literal)
   float arg = 0.0f;
-  for (long long k = 0; k < n; ++k) {
-    const float v = x[k];
+  // one step of the recurrence (src/filter.cpp:188-219)
+  auto pll_step = [&](float v) __attribute__((always_inline)) {
     const float eI = (v == 0.0f ? 1.0f : v) * fbI;
     const float eQ = v * (-1.0f * fbQ);
     const float eD = (float)atan2((double)eQ, (double)eI);
@@ -59,6 +59,40 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     sincos((double)arg, &sv, &cv);  // one argument reduction for both (same values as sin() and cos())
     fbI = (float)cv;
     fbQ = (float)sv;
+  };
+  // The chain is latency-bound (one lane per stream).  Inputs are loaded one
+  // chunk ahead into registers, so no step waits on memory: a per-sample
+  // load put a full load latency -- and the previous step's store, which
+  // shares the vmcnt counter -- into every step.
+  constexpr int CH = 8;
+  const long long nc = n / CH * CH;
+  float xa[CH], xb[CH];
+  auto load = [&](float (&buf)[CH], long long k) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) buf[j] = x[k + j];
+    // keep the loads here: left to the scheduler they sink to their use
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto run = [&](const float (&buf)[CH], long long k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      pll_step(buf[j]);
+      if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
+    }
+  };
+  // ping-pong register chunks (no copies, so no wait at the chunk boundary
+  // beyond the chunk being consumed); a chunk past nc re-loads an in-bounds one
+  if (nc > 0) load(xa, 0);
+  for (long long k0 = 0; k0 < nc; k0 += 2 * CH) {
+    load(xb, k0 + CH < nc ? k0 + CH : k0);
+    run(xa, k0);
+    if (k0 + CH < nc) {
+      load(xa, k0 + 2 * CH < nc ? k0 + 2 * CH : k0);
+      run(xb, k0 + CH);
+    }
+  }
+  for (long long k = nc; k < n; ++k) {  // ragged tail
+    pll_step(x[k]);
     if (k + 1 < n) ar[k + 1] = arg;
   }
   st[0] = fbI;

@@ -447,16 +447,17 @@ def test_preconditions_are_errors(gpu_ctx, built_lib):
         gpu_ctx.fm_demod(np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(2, np.float32))
 
 
-@pytest.mark.parametrize("mix", [False, True])
-def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix):
+@pytest.mark.parametrize("mix,n", [(False, 12000), (True, 12000), (False, 1003), (True, 5)])
+def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix, n):
     """fmPLL (src/filter.cpp:174-228), one lane per stream, against the
     oracle on 192 streams x 2 blocks x 12,000 samples (~18M double-precision
     atan2/cos/sin evaluations): every NCO sample and all six state floats
     bit-equal.  Pilots: 19 kHz tones at 240 kHz with random phase, frequency
-    offset, amplitude and noise, plus exact zeros (the `PLLin == 0` branch)."""
+    offset, amplitude and noise, plus exact zeros (the `PLLin == 0` branch).
+    n = 1003 and 5 take the kernel's ragged tail (its chunks are 8 samples)."""
     sdrhip = built_lib
-    rng = np.random.default_rng(19000 + mix)
-    S, n, Fs = 192, 12000, 240e3
+    rng = np.random.default_rng(19000 + mix + n)
+    S, Fs = 192, 240e3
     t = np.arange(2 * n)
     f = 19e3 + rng.uniform(-40, 40, S)[:, None]
     x = (rng.uniform(0.01, 0.3, S)[:, None] * np.cos(2 * np.pi * f / Fs * t + rng.uniform(0, 6.3, S)[:, None])
