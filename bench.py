@@ -57,6 +57,10 @@ CONFIGS = {
     # SURVEY 8(f) 2 (stereo half): the whole mode-0 stereo path, PLL one lane per stream
     "stereo0": dict(kind="stereo_u8", D=10, up=1, down=5, ntaps=101, n=51200, streams=1024,
                     workload="mode0_stereo_u8iq_to_s16pcm_LR_block51200"),
+    # the same with 16x the streams: the PLL recurrence is latency-bound per stream (one lane
+    # each), so 1,024 streams occupy 16 waves of the chip; more streams per step fill it
+    "stereo0w": dict(kind="stereo_u8", D=10, up=1, down=5, ntaps=101, n=51200, streams=16384,
+                     workload="mode0_stereo_u8iq_to_s16pcm_LR_block51200_16k_streams"),
     # BASELINE config 5's fp16 arm: fp16 storage, fp32 accumulation (v_dot2_f32_f16); not
     # bit-exact -- the line carries its error against the exact fp32 path
     "cfg5h": dict(kind="fir_block_f16", D=1, ntaps=1024, n=1048576, streams=2,
