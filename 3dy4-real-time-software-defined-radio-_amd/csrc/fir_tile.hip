@@ -58,6 +58,11 @@
 #ifndef SDR_NPASS
 #define SDR_NPASS 3
 #endif
+// SDR_OUT_NT: non-temporal hint on the demod output stores of the f32 path
+// (warm same-box A/B: f32 -1..2 %, u8 neutral -> f32 only)
+#ifndef SDR_OUT_NT
+#define SDR_OUT_NT 1
+#endif
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
@@ -725,7 +730,12 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       if (lane >= 1 && (a.ablate != 3 || d[0] == 12345.0f)) {
         if (vec && m0 + R <= nout) {
           if constexpr (R == 2) {
-            *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);
+            if constexpr (SDR_OUT_NT && SRC == Src::F32) {
+              typedef float f2 __attribute__((ext_vector_type(2)));
+              __builtin_nontemporal_store(f2{d[0], d[1]}, reinterpret_cast<f2*>(o + m0));
+            } else {
+              *reinterpret_cast<float2*>(o + m0) = make_float2(d[0], d[1]);
+            }
           } else if constexpr (R == 4) {
             *reinterpret_cast<float4*>(o + m0) = make_float4(d[0], d[1], d[2], d[3]);
           } else {
