@@ -4,7 +4,9 @@
 // drop-in filter.h implementation, and the device-resident batched calls.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -111,6 +113,27 @@ bool vec_ok(const void* p, long long stride_elems, int elem_bytes, int nstreams,
 }
 
 }  // namespace
+
+// ------------------------------------------------------- launch helpers --
+namespace sdr {
+int device_cu_count() {
+  // one slot per device, written once with the same value by whichever
+  // thread gets there first (relaxed atomics: no torn or racy reads)
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+}  // namespace sdr
 
 extern "C" {
 
@@ -301,6 +324,60 @@ int sdr_event_destroy(sdr_ctx* c, sdr_event* ev) {
     hipError_t h = hipEventDestroy(ev->ev);
     delete ev;
     if (h != hipSuccess) return hip_fail(c, h, "hipEventDestroy");
+  }
+  return SDR_OK;
+}
+
+// Stream capture -> instantiated HIP graph -> stream-ordered replay: a
+// caller's per-block launch sequence (the mono/stereo pipelines' ~10
+// launches per block, bench.py's steps) becomes one launch.  Thread-local
+// capture mode, so other host threads (other devices' contexts) keep
+// working while this one records.
+struct sdr_graph {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+int sdr_graph_begin(sdr_ctx* c) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!c->cur) return fail(c, SDR_EINVAL, "graph capture needs a non-null stream");
+  SDR_HIP(c, hipStreamBeginCapture(c->cur, hipStreamCaptureModeThreadLocal));
+  return SDR_OK;
+}
+
+int sdr_graph_end(sdr_ctx* c, sdr_graph** out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!out) return fail(c, SDR_EINVAL, "null graph");
+  *out = nullptr;
+  auto* g = new sdr_graph;
+  hipError_t h = hipStreamEndCapture(c->cur, &g->g);
+  if (h == hipSuccess) h = hipGraphInstantiate(&g->exec, g->g, nullptr, nullptr, 0);
+  if (h != hipSuccess) {
+    if (g->g) (void)hipGraphDestroy(g->g);
+    delete g;
+    return hip_fail(c, h, "stream capture");
+  }
+  *out = g;
+  return SDR_OK;
+}
+
+int sdr_graph_launch(sdr_ctx* c, sdr_graph* g) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!g) return fail(c, SDR_EINVAL, "null graph");
+  SDR_HIP(c, hipGraphLaunch(g->exec, c->cur));
+  return SDR_OK;
+}
+
+int sdr_graph_destroy(sdr_ctx* c, sdr_graph* g) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (g) {
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->g) (void)hipGraphDestroy(g->g);
+    delete g;
   }
   return SDR_OK;
 }

@@ -336,26 +336,6 @@ __device__ __forceinline__ void stage_store(float* lds0, float* lds1, int tid,
   if (G::REM && tid < G::REM) put(tid + G::FULL * G::NTH, v0[G::FULL], v1[G::FULL]);
 }
 
-// Split mode, u8 wire: store channel 0 (bytes 0, 2 of each raw word) to
-// `buf` and unpack channel 1 (bytes 1, 3) into v1 as floats, which frees v0
-// for the next tile's raw prefetch before channel 0 is scanned.
-template <int D, int T, int R, bool DEMOD, int NW>
-__device__ __forceinline__ void stage_u8_split(float* buf, int tid,
-                                               const float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
-                                               float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
-  using G = Geom<D, T, R, DEMOD, NW>;
-#pragma unroll
-  for (int it = 0; it <= G::FULL; ++it) {
-    if (it == G::FULL && !G::REM) break;
-    const uint32_t bx = __float_as_uint(v0[it].x), by = __float_as_uint(v0[it].y);
-    const int i = tid + it * G::NTH;
-    if (it < G::FULL || tid < G::REM)
-      *reinterpret_cast<float4*>(buf + 4 * i) = make_float4(u8_byte_to_f32<0>(bx), u8_byte_to_f32<2>(bx),
-                                                            u8_byte_to_f32<0>(by), u8_byte_to_f32<2>(by));
-    v1[it] = make_float4(u8_byte_to_f32<1>(bx), u8_byte_to_f32<3>(bx), u8_byte_to_f32<1>(by), u8_byte_to_f32<3>(by));
-  }
-}
-
 // f(integral_constant<int, B>), f(<B+1>), ..., f(<E-1>): a fully unrolled
 // loop whose index is a constant expression in the body.
 template <int B, int E, class F>
@@ -366,32 +346,26 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// TM = where the taps live: 0 LDS broadcast rows, 1 SGPRs (NPASS passes).
-// PF = prefetch depth: tile i+PF's loads are issued (into one of PF
-// register sets) before tile i is computed.
+// TM = where the taps live: 0 LDS broadcast rows (D = 1), 1 SGPRs (NPASS
+// passes).  The loads of tile i+1 are issued into registers before tile i is
+// computed (prefetch depth 1).
 // FMA = the fused multiply-add arithmetic mode (SDR_ARITH_FMA, SGPR taps
 // only): same taps, same order, one rounding per tap instead of two -- not
 // the reference's bits, within the fp32 tolerance of DESIGN.md 2.
-// SPLIT = one LDS buffer: channel 0 is staged and scanned, then channel 1
-// (NCH == 2, SGPR taps, prefetch depth 1).  Half the LDS per wave, so the
-// VGPRs, not the LDS, set the occupancy (14 -> 16 waves per CU at D = 10).
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, int PF, bool FMA = false,
-          bool SPLIT = false>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
-  static_assert(PF == 1 || PF == 2, "prefetch depth");
   using G = Geom<D, T, R, DEMOD, NW>;
   constexpr int NTH = G::NTH;
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
   static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
+  static_assert(!FMA || TM == 1, "FMA mode: SGPR taps");
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lds0 = smem;
-  static_assert(!SPLIT || (NCH == 2 && TM == 1 && PF == 1), "split mode: 2 channels, SGPR taps, prefetch 1");
-  static_assert(!SPLIT || 2 * G::STRIP <= G::LDS_LEN, "split mode: both strips in the one buffer");
-  float* lds1 = SPLIT ? smem : smem + G::LDS_LEN;
-  float* htab = smem + 2 * G::LDS_LEN;                 // R tap rows (TM 0)
-  float* strip0 = lds0;  // the block's last inputs (tile 0, after its scan)
-  float* strip1 = SPLIT ? smem + G::STRIP : lds1;
+  float* lds1 = smem + G::LDS_LEN;
+  float* htab = smem + 2 * G::LDS_LEN;  // R tap rows (TM 0)
+  float* strip0 = lds0;                 // the block's last inputs (tile 0, after its scan)
+  float* strip1 = lds1;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -431,15 +405,11 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   }
 
   using Stage = float4[G::FULL + 1];
-  Stage sa0, sa1, sb0, sb1;
+  Stage sa0, sa1;
 #pragma unroll
-  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = sb0[i] = sb1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.ablate != 1) {
+  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.ablate != 1)
     stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
-    if (PF == 2 && first + step < last)
-      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first + step), n, tid, sb0,
-                                               sb1);
-  }
 
   auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
     const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
@@ -471,18 +441,15 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // stages the block's last STRIP inputs (old state where p < 0: the
     // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
     // rewrites the state below.
-    if constexpr (!SPLIT) {
+    __syncthreads();
+    stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
+    if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
-      stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
-      if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
-        __syncthreads();
-        edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, false, strip0, strip1);
-      }
-      __syncthreads();
-      if (lin + PF * step < last && a.ablate != 1)
-        stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + PF * step), n, tid,
-                                                 v0, v1);
+      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, false, strip0, strip1);
     }
+    __syncthreads();
+    if (lin + step < last && a.ablate != 1)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + step), n, tid, v0, v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
@@ -502,95 +469,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       acc0[r] = 0.0f;
       acc1[r] = 0.0f;
     }
-    if constexpr (SPLIT) {
-      // One channel at a time through the single buffer lds0 (== lds1):
-      //   store ch0 -> [edge ch0] -> prefetch next ch0 -> scan ch0 ->
-      //   store ch1 -> [edge ch1] -> prefetch next ch1 -> scan ch1.
-      // u8: the raw words carry both channels; ch1 is unpacked into v1 at
-      // the ch0 store, so the next tile's raw prefetch can go into v0 then.
-      const bool edge = tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n);  // workgroup-uniform
-      const bool more = lin + step < last && a.ablate != 1;
-      const TileRef tn = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, more ? lin + step : lin);
-      TileRef tq = tr;  // channel 1 seen as channel 0
-      tq.x0 = tr.x1;
-      tq.st0 = tr.st1;
-      // single-channel scan, SGPR taps in NPASS passes (as below)
-      auto scan1 = [&](const float* w, float (&acc)[R]) __attribute__((always_inline)) {
-        constexpr int NPASS = SDR_NPASS, KP = (T + NPASS - 1) / NPASS;
-        using hconst = const __attribute__((address_space(4))) float*;
-        const hconst hc = (hconst)h;
-        float hs[KP];
-        static_for<0, NPASS>([&](auto pi) {
-          constexpr int k0 = decltype(pi)::value * KP;
-          constexpr int k1 = k0 + KP < T ? k0 + KP : T;
-#pragma unroll
-          for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
-#pragma unroll
-          for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
-          constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
-          constexpr int whi = G::HALO + D * (R - 1) - k0;
-          constexpr int clo = wlo / 4, chi = whi / 4;
-          float4 q = *reinterpret_cast<const float4*>(w + 4 * chi);
-          static_for<0, chi - clo + 1>([&](auto ci) {
-            constexpr int c = chi - decltype(ci)::value;
-            float4 nq = q;
-            if constexpr (c > clo) nq = *reinterpret_cast<const float4*>(w + 4 * (c - 1));
-            const float e[4] = {q.x, q.y, q.z, q.w};
-            static_for<0, 4>([&](auto ji) {
-              constexpr int j = 3 - decltype(ji)::value;
-              static_for<0, R>([&](auto ri) {
-                constexpr int r = decltype(ri)::value;
-                constexpr int k = G::HALO + D * r - (4 * c + j);
-                if constexpr (k >= k0 && k < k1) {
-                  if constexpr (FMA)
-                    acc[r] = __builtin_fmaf(hs[k - k0], e[j], acc[r]);
-                  else
-                    acc[r] = acc[r] + hs[k - k0] * e[j];
-                }
-              });
-            });
-            q = nq;
-#pragma unroll
-            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
-            __builtin_amdgcn_sched_barrier(0);
-          });
-        });
-      };
-      // ---- channel 0
-      __syncthreads();
-      if constexpr (SRC == Src::U8)
-        stage_u8_split<D, T, R, DEMOD, NW>(lds0, tid, v0, v1);
-      else
-        stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds0, lds0, tid, v0, v0);
-      if (edge) {
-        __syncthreads();
-        edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, tid, n, ns, lds0, lds0, false, strip0, strip1, 0);
-      }
-      __syncthreads();
-      if (more) {
-        if constexpr (SRC == Src::U8)
-          stage_load<D, T, R, DEMOD, NW, 2, SRC>(tn, n, tid, v0, v0);  // raw words of both channels
-        else
-          stage_load<D, T, R, DEMOD, NW, 1, SRC>(tn, n, tid, v0, v0);
-      }
-      scan1(lds0 + lbase, acc0);
-      // ---- channel 1
-      __syncthreads();
-      stage_store<D, T, R, DEMOD, NW, 1, Src::F32>(lds0, lds0, tid, v1, v1);
-      if (edge) {
-        __syncthreads();
-        edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tq, tid, n, ns, lds0, lds0, false, strip0, strip1, 1);
-      }
-      __syncthreads();
-      if constexpr (SRC == Src::F32) {
-        if (more) {
-          TileRef tnq = tn;
-          tnq.x0 = tn.x1;
-          stage_load<D, T, R, DEMOD, NW, 1, SRC>(tnq, n, tid, v1, v1);
-        }
-      }
-      scan1(lds0 + lbase, acc1);
-    } else if (a.ablate == 2) {
+    if (a.ablate == 2) {
       acc0[0] = lds0[lbase];
       acc1[0] = lds1[lbase];
     } else {
@@ -830,12 +709,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     }
   };
 
-  for (int lin = first; lin < last; lin += PF * step) {
-    tile(lin, sa0, sa1);
-    if constexpr (PF == 2) {
-      if (lin + step < last) tile(lin + step, sb0, sb1);
-    }
-  }
+  for (int lin = first; lin < last; lin += step) tile(lin, sa0, sa1);
 }
 
 // ---------------------------------------------------------- generic path --
@@ -911,8 +785,7 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 // ------------------------------------------------------------ dispatch ----
 // Persistent grid: about `wpc` waves per CU (or the tile count, if smaller),
 // each workgroup walking its share of the tiles (see `walk` in fir_tile).
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM = 0, int PF = 1, bool FMA = false,
-          bool SPLIT = false>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
@@ -920,21 +793,10 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
   a.tiles_per_stream = (int)((nout + G::ADV - 1) / G::ADV);
   const long long total = (long long)a.tiles_per_stream * a.nstreams;
   if (total <= 0 || total > 0x7fffffffLL) return hipErrorInvalidValue;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
-  static const int per_cu_env = [] {
-    const char* e = std::getenv("SDR_WG_PER_CU");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int ncu = device_cu_count();
+  static const int per_cu_env = env_int("SDR_WG_PER_CU", 0);
   const int per_cu = per_cu_env > 0 ? per_cu_env : wpc;
-  static const int walk = [] {
-    const char* e = std::getenv("SDR_TILE_WALK");
-    return e ? std::atoi(e) : 1;
-  }();
+  static const int walk = env_int("SDR_TILE_WALK", 1);
   const long long slots = (long long)ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
   long long blocks;
   if (walk == 1 && total >= 8 * 8) {
@@ -950,62 +812,29 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
     a.tiles_per_wg = (int)((total + grid - 1) / grid);
     blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
   }
-  static const int ablate = [] {
-    const char* e = std::getenv("SDR_ABLATE");
-    return e ? std::atoi(e) : 0;
-  }();
+  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
   a.ablate = ablate;
-  static const int lds_pad = [] {  // timing experiments only: extra LDS per workgroup (occupancy sweep)
-    const char* e = std::getenv("SDR_LDS_PAD");
-    return e ? std::atoi(e) : 0;
-  }();
-  const size_t lds = (size_t)(SPLIT ? G::LDS_LEN : G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float) +
-                     lds_pad;  // TM 1: no tap rows; SPLIT: one channel buffer
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, PF, FMA, SPLIT>), dim3((unsigned)blocks), dim3(G::NTH), lds, st, a, h);
+  const size_t lds = (size_t)(G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float);  // TM 1: no tap rows
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st,
+                     a, h);
   return hipGetLastError();
 }
 
-// Fast-path table: (R outputs per lane, NW waves per workgroup, tap mode,
-// prefetch depth, waves per CU) per decimation factor and input format.
-// D*R must be a multiple of 4 (aligned lane windows).  The defaults are the
-// measured best on MI355X; SDR_FIR_VARIANT=<R>x<NW>[r|p] (no
-// suffix: LDS tap rows; r: SGPR taps; p: SGPR taps + 2-deep prefetch) and
-// SDR_WG_PER_CU override them for experiments.
+// Tile shape per decimation factor: R outputs per lane, one wave per
+// workgroup, taps in SGPRs (TM 1) or LDS rows (TM 0), waves per CU.  D*R must
+// be a multiple of 4 (aligned lane windows).  These are the measured best on
+// MI355X (where the variants that lost are listed).
 struct Variant {
-  int R, NW, tm, pf, wpc;  // tm: taps in LDS rows (0) or SGPRs (1); pf: prefetch depth
-  int split = 0;           // fused 2-channel: one LDS buffer, channels in turn (fir_tile SPLIT)
+  int R, NW, tm, wpc;
 };
 
-Variant variant_for_default(int D, bool demod, Src src);
-
 Variant variant_for(int D, bool demod, Src src) {
-  static const char* env = std::getenv("SDR_FIR_VARIANT");
-  if (env) {
-    int r = 0, w = 0;
-    char m = 0;
-    const int got = std::sscanf(env, "%dx%d%c", &r, &w, &m);
-    if (got >= 2) {
-      // suffix s: SGPR taps, prefetch 1, split channels (fused D = 10 / 5, one wave)
-      const Variant v{r, w, m == 'r' || m == 'p' || m == 's' ? 1 : 0, m == 'p' ? 2 : 1, m == 'p' ? 24 : 32, m == 's'};
-      if (v.split && !(demod && w == 1 && ((D == 10 && r == 2) || (D == 5 && r == 4)))) return variant_for_default(D, demod, src);
-      const bool known = (D == 10 && ((r == 2 && (w == 1 || w == 2 || w == 4)) || (r == 4 && (w == 1 || w == 2)))) ||
-                         (D == 5 && r == 4 && (w == 1 || w == 4)) ||
-                         (D == 1 && !demod && ((r == 4 && (w == 1 || w == 4)) || (r == 8 && w == 1)));
-      if (known) return v;
-    }
-  }
-  return variant_for_default(D, demod, src);
-}
-
-Variant variant_for_default(int D, bool demod, Src src) {
   switch (D) {
-    // f32 fused: prefetch depth 1 (≈115 VGPRs, 4 waves/SIMD) and 64 one-wave
-    // workgroups per CU beat depth 2 (165 VGPRs, 3 waves/SIMD) by 4-6 % once
-    // the clock has ramped (same-box A/B)
-    case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 1, 64} : Variant{2, 1, 1, 1, 32};
-    case 5: return {4, 1, 1, 1, 32};
-    case 1: return {4, 1, 0, 1, 32};
-    default: return {0, 0, 0, 1, 32};
+    // f32 fused: 64 one-wave workgroups per CU
+    case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 64} : Variant{2, 1, 1, 32};
+    case 5: return {4, 1, 1, 32};
+    case 1: return {4, 1, 0, 32};
+    default: return {0, 0, 0, 32};
   }
 }
 
@@ -1023,63 +852,24 @@ template <int NCH, bool DEMOD, Src SRC>
 hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, bool* handled) {
   *handled = true;
   const Variant v = variant_for(a.D, DEMOD, SRC);
-  const int key = a.D * 10000 + v.R * 100 + v.NW;
   if (a.ntaps == 101) {
     if constexpr (DEMOD) {
-      if (v.split) {
-        switch (key * 10 + (a.fma ? 1 : 0)) {
-          case 1002010: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 1, false, true>(a, h, st, v.wpc);
-          case 1002011: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 1, true, true>(a, h, st, v.wpc);
-          case 504010: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, 1, false, true>(a, h, st, v.wpc);
-          case 504011: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, 1, true, true>(a, h, st, v.wpc);
-          default: break;
-        }
-      }
-    }
-    // SDR_ARITH_FMA: instantiated for the default fused variants (D = 10 and
-    // 5); any other shape runs the exact arithmetic (inside the tolerance)
-    if constexpr (DEMOD) {
-      if (a.fma && v.tm == 1) {
-        switch (key * 10 + v.pf) {
-          case 1002012:
-            if constexpr (SRC == Src::F32) return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 2, true>(a, h, st, v.wpc);
-            break;
-          case 1002011: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 1, true>(a, h, st, v.wpc);
-          case 504011: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, 1, true>(a, h, st, v.wpc);
-          default: break;
-        }
-      }
-    }
-    if (v.pf == 2) {
-      switch (key) {
-        case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, 2>(a, h, st, v.wpc);
+      // SDR_ARITH_FMA: instantiated for the fused kernels; any other shape
+      // runs the exact arithmetic (inside the tolerance)
+      switch (a.D) {
+        case 10:
+          return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, v.wpc)
+                       : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 5:
+          return a.fma ? run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, v.wpc)
+                       : run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         default: break;
       }
-    }
-    if (v.tm == 1) {
-      switch (key) {
-        case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 100202: return run_tile<10, 101, 2, 2, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        default: break;
-      }
-    }
-    switch (key) {
-      case 100201: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-      case 100204: return run_tile<10, 101, 2, 4, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-      case 100401: return run_tile<10, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-      case 100402: return run_tile<10, 101, 4, 2, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-      case 50401: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-      case 50404: return run_tile<5, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-      default: break;
-    }
-    if constexpr (!DEMOD && NCH == 1) {
-      switch (key) {
-        case 10401: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-        case 10404: return run_tile<1, 101, 4, 4, NCH, DEMOD, SRC>(a, h, st, v.wpc);
-        case 10801: return run_tile<1, 101, 8, 1, NCH, DEMOD, SRC>(a, h, st, v.wpc);
+    } else if constexpr (NCH == 1) {
+      switch (a.D) {
+        case 10: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 5: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 1: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC, 0>(a, h, st, v.wpc);
         default: break;
       }
     }
@@ -1110,7 +900,6 @@ hipError_t launch_demod(const float* I, const float* Q, long long n, int nstream
 // hold decimated I/Q when a demod launch takes the generic path.
 hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, Src src, hipStream_t st,
                       float* scratch_y0, float* scratch_y1, bool allow_fast) {
-  if (allow_fast && !a.fma && fir_stream_ok(a.D, a.ntaps, a.ns, demod, nch, src)) return launch_fir_stream(a, h, st);
   if (allow_fast && fir_has_fast_path(a.D, a.ntaps, a.ns, nch, demod, src)) {
     bool handled = false;
     hipError_t e = hipSuccess;

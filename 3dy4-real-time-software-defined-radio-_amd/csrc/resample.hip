@@ -374,20 +374,11 @@ hipError_t launch_resample(int up, int down, const float* x, long long n, int ns
     if ((segpad / 4) % 2 == 0) segpad += 4;
     a.segpad = segpad;
     a.vec = (down % 4 == 0) && x_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    static const int ablate = [] {
-      const char* e = std::getenv("SDR_ABLATE");
-      return e ? std::atoi(e) : 0;
-    }();
+    static const int ablate = env_int("SDR_ABLATE", 0);
     a.ablate = ablate;
     const long long seglen_max = qspan + cnt_max + 3;  // one DMA wave-instruction per column
     if (segpad <= kPPSeg && seglen_max <= 256 && a.vec) {
-      static int ncu = 0;
-      if (!ncu) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-          ncu = 256;
-      }
+      const int ncu = device_cu_count();
       const long long ncb = (a.ncols + kPPLanes - 1) / kPPLanes;
       long long slots = ncu / a.nphg;  // ~one workgroup per CU
       if (slots < 1) slots = 1;

@@ -604,16 +604,8 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
   const long long step = ((long long)kRsPG * down + up - 1) / up + 8;
   if (!use_lp && (!rs_enabled() || span + step > kRsRing)) return false;
-  static const int ablate = [] {
-    const char* v = std::getenv("SDR_ABLATE");
-    return v ? std::atoi(v) : 0;
-  }();
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
+  static const int ablate = env_int("SDR_ABLATE", 0);
+  const int ncu = device_cu_count();
   const int np = (int)((ny + up - 1) / up);
   if (use_lp) {
     // columns per item: S*K chains, bounded by the staging buffer

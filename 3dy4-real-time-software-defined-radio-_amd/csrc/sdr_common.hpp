@@ -60,6 +60,13 @@ __device__ __forceinline__ float u8_byte_to_f32(uint32_t w) {
   return __builtin_fmaf((float)((w >> (8 * B)) & 0xffu), 0.0078125f, -1.0f);
 }
 
+// Compute units of the calling thread's current device, cached per device
+// (the launchers run concurrently from several host threads: the drop-in's
+// two threads per block, bench.py's one thread per GPU).
+int device_cu_count();
+// Integer environment switch (timing experiments), `dflt` when unset.
+int env_int(const char* name, int dflt);
+
 // Host-side launchers, one per kernel family (defined next to the kernels).
 // allow_fast = false forces the generic kernel (misaligned buffers).
 hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, Src src, hipStream_t st,
@@ -107,10 +114,6 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
                              void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
                              hipStream_t st);
 hipError_t launch_f32_to_f16(const float* x, long long count, void* y, hipStream_t st);
-
-// Loader/consumer front-end engine (fir_stream.hip): fused f32 D = 10, T = 101.
-bool fir_stream_ok(int D, int ntaps, int ns, bool demod, int nch, Src src);
-hipError_t launch_fir_stream(const FirLaunch& a, const float* h, hipStream_t st);
 
 // Whether the tiled fast path handles (D, ntaps, ns) for this source; false
 // means launch_fir takes the generic path (still exact, slower).

@@ -67,6 +67,10 @@ _SIGS = {
     "sdr_event_record": [_vp, _vp],
     "sdr_event_synchronize": [_vp, _vp],
     "sdr_event_destroy": [_vp, _vp],
+    "sdr_graph_begin": [_vp],
+    "sdr_graph_end": [_vp, C.POINTER(_vp)],
+    "sdr_graph_launch": [_vp, _vp],
+    "sdr_graph_destroy": [_vp, _vp],
     "sdr_resample_out_len": [_i, _i, _ll],
     "sdr_taps_lpf": [C.c_float, C.c_float, _i, _i, _vp],
     "sdr_taps_bpf": [C.c_float, C.c_float, C.c_float, _i, _i, _vp],
@@ -188,6 +192,21 @@ def _inplace(a, what):
     return a
 
 
+class Graph:
+    """An instantiated capture (sdr_graph): launch() replays it."""
+
+    def __init__(self, ctx: "Context", g):
+        self._ctx, self._g = ctx, g
+
+    def launch(self):
+        self._ctx._check(lib().sdr_graph_launch(self._ctx._c, self._g), "graph_launch")
+
+    def close(self):
+        if self._g:
+            lib().sdr_graph_destroy(self._ctx._c, self._g)
+            self._g = _vp()
+
+
 class Context:
     """One GPU + one HIP stream + scratch buffers (sdr_ctx)."""
 
@@ -231,6 +250,20 @@ class Context:
 
     def synchronize(self):
         self._check(lib().sdr_ctx_synchronize(self._c), "synchronize")
+
+    # -- HIP-graph capture of this context's stream (sdr_graph_*)
+    def capture(self, fn) -> "Graph":
+        """Record the stream-ordered calls `fn()` makes on this context into
+        a HIP graph (nothing runs while recording); Graph.launch() replays
+        them on the context's stream."""
+        self._check(lib().sdr_graph_begin(self._c), "graph_begin")
+        g = _vp()
+        try:
+            fn()
+        finally:
+            rc = lib().sdr_graph_end(self._c, C.byref(g))
+        self._check(rc, "graph_end")
+        return Graph(self, g)
 
     def last_error(self) -> str:
         return lib().sdr_ctx_last_error(self._c).decode()

@@ -12,9 +12,14 @@ The path shards with no data-path collective:
   for bit, src/filter.cpp:82/139 carry the raw input tail), so a segment
   starting at sample p0 (a multiple of D) is computed exactly by a rank that
   is handed (a) the ns input samples before p0 as its ``state`` and (b) the
-  decimated I/Q sample just before p0 as its ``prev``.  Both are *replicated
-  reads* of the previous segment's data (a halo of ns + T - 1 + D samples),
-  not messages: no RCCL/xGMI traffic.
+  decimated I/Q sample just before p0 as its ``prev``.  (b) is output
+  p0/D - 1, the last output of one FIR+decimate call over [halo_lo, p0)
+  with the ns samples before halo_lo as that call's state.  halo_lo =
+  p0 - D*ceil(ns/D) is a multiple of D (the call runs at the stream's own
+  decimation phase) and leaves the call >= ns inputs (the reference's
+  n >= ns precondition).  The rank therefore reads a halo of
+  D*ceil(ns/D) + ns samples before p0 -- replicated reads of the previous
+  segment's data, not messages: no RCCL/xGMI traffic.
 """
 from __future__ import annotations
 
@@ -35,9 +40,10 @@ def streams_of(rank: int, nstreams: int, world: int) -> list[int]:
 @dataclass(frozen=True)
 class Segment:
     rank: int
-    start: int      # first input sample of the segment (multiple of D)
+    start: int      # first input sample of the segment (p0, a multiple of D)
     stop: int       # one past the last input sample
-    halo_lo: int    # first input sample the rank must also read (state + prev halo)
+    halo_lo: int    # first input of the prev_* recompute call (p0 - D*ceil(ns/D)); 0 for the first segment
+    read_lo: int    # first input sample the rank reads: the recompute call's state (halo_lo - ns, >= 0)
 
     @property
     def length(self) -> int:
@@ -50,6 +56,8 @@ def segment_plan(n: int, D: int, ntaps: int, ns: int, world: int) -> list[Segmen
     reference's n >= ns precondition) and with its halo range."""
     if n % D:
         raise ValueError("n must be a multiple of D")
+    if ns < ntaps - 1:
+        raise ValueError("state shorter than ntaps - 1")
     nout = n // D
     bounds = [round(nout * r / world) * D for r in range(world + 1)]
     segs = []
@@ -57,6 +65,6 @@ def segment_plan(n: int, D: int, ntaps: int, ns: int, world: int) -> list[Segmen
         a, b = bounds[r], bounds[r + 1]
         if b - a < max(ns, D):
             raise ValueError(f"segment {r} too short ({b - a} < {max(ns, D)})")
-        halo = a - max(ns, D + ntaps - 1)  # state tail + the taps of the output before `a`
-        segs.append(Segment(rank=r, start=a, stop=b, halo_lo=max(halo, 0) if a else 0))
+        halo_lo = max(a - D * (-(-max(ns, 1) // D)), 0) if a else 0
+        segs.append(Segment(rank=r, start=a, stop=b, halo_lo=halo_lo, read_lo=max(halo_lo - ns, 0) if a else 0))
     return segs

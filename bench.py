@@ -8,23 +8,38 @@ blocks of 65,540 IQ pairs (65,536 rounded up to a multiple of 10, the
 reference's own precondition), fp32 planar I/Q resident in HBM.  One step =
 the next block of each of 1024 independent synthetic streams (state carried
 across steps exactly as the reference carries it between blocks), i.e. one
-batched launch of the fused kernel over 67.1 M IQ pairs.
+batched launch of the fused kernel over 67.1 M IQ pairs.  The steps cycle
+over --batches distinct input batches (2 by default: 1.07 GB for cfg2, four
+times the 256 MiB Infinity Cache), so no step re-reads a batch the previous
+one left on chip.
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank runs
-its own 1024 streams (weak scaling, no data-path collective -- the streams
-are independent); the only collectives are the timing barrier and the
-max-over-ranks of the elapsed time.
+Multi-GPU: the streams are independent, so every GPU runs
+its own streams (weak scaling) and nothing is exchanged -- no RCCL anywhere.
+  * ``python bench.py --gpus N`` runs the N devices from ONE process, one
+    persistent host thread per device (its own sdr context, HIP stream and
+    on-device synthetic input), started together from a host barrier; each
+    device is timed with HIP events on its own stream; the aggregate is all
+    devices' IQ pairs / the slowest device's time.
+  * under ``torch.distributed.run`` (WORLD_SIZE set) every rank runs one
+    device (LOCAL_RANK); the timing barrier and the max-over-ranks reduction
+    go over a CPU ``gloo`` group -- again no device collective.
 
-Prints ONE JSON line (rank 0).  Other workloads: --config cfg2u8 (u8 wire
-input fused in), cfg3 (polyphase resampler 147/800, 151 taps/phase),
-cfg4 (8 long streams x 32 x 262,150-pair blocks per GPU), cfg5 (1024-tap
-FIR, no decimation).
+Timed steps are replayed from a HIP graph of --graph-steps steps (the
+library's sdr_graph_* capture of the same calls), so N host threads never
+bound the launch rate; --no-graph launches them one by one.
+
+Prints ONE JSON line.  Other workloads: --config cfg2u8 (u8 wire input
+fused in), cfg3 (polyphase resampler 147/800, 151 taps/phase), cfg4 (one
+long stream per GPU, 256 x 262,150-pair blocks per step), cfg4x8 (8 streams
+per GPU x 32 blocks), cfg5/cfg5h (1024-tap FIR, fp32 / fp16 storage), mono0,
+stereo0, stereo0w (the reference program's mode-0 paths on the device).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -46,8 +61,12 @@ CONFIGS = {
                    workload="fir101_dec10_fmdemod_u8wire_block65540"),
     "cfg3": dict(kind="resample", up=147, down=800, ntaps=151 * 147, n=65600, streams=1024,
                  workload="polyphase_resampler_147_800_151pp_block65600"),
-    "cfg4": dict(kind="frontend_f32", D=10, ntaps=101, n=262150 * 32, streams=8,
-                 workload="fir101_dec10_fmdemod_f32_8streams_x32blocks_of_262150"),
+    # BASELINE config 4: one independent stream per GPU; a step is 256 consecutive
+    # 262,150-pair blocks of it in one call (block-size independence, src/filter.cpp:139)
+    "cfg4": dict(kind="frontend_f32", D=10, ntaps=101, n=262150 * 256, streams=1,
+                 workload="fir101_dec10_fmdemod_f32_1stream_x256blocks_of_262150"),
+    "cfg4x8": dict(kind="frontend_f32", D=10, ntaps=101, n=262150 * 32, streams=8,
+                   workload="fir101_dec10_fmdemod_f32_8streams_x32blocks_of_262150"),
     "cfg5": dict(kind="fir_block", D=1, ntaps=1024, n=1048576, streams=2,
                  workload="fir1024_block1M_f32_IandQ"),
     # SURVEY 8(f) 2+4: the reference program's whole mono path (mode 0) on the device,
@@ -68,7 +87,7 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -82,65 +101,74 @@ def parse():
     ap.add_argument("--arith", choices=("exact", "fma"), default=os.environ.get("SDR_BENCH_ARITH", "exact"),
                     help="front-end FIR arithmetic: the reference's bits (exact) or one fused multiply-add per tap "
                          "(fma, tolerance-tested)")
-    return ap.parse_args()
+    ap.add_argument("--batches", type=int, default=2, help="distinct input batches the steps cycle over")
+    ap.add_argument("--graph-steps", type=int, default=10, help="steps per replayed HIP graph")
+    ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(seconds: float):
-    """The reference's own front end (oracle/_ref, kind 'reference') or, if it
-    was not built, the bit-exact C restatement (kind 'port'), timed on this
-    host's cores over a bounded sample of the same workload: 65,540-pair
-    mode-0 blocks, one independent stream per thread."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as orc
-    from sdrhip.synth import fm_planar
+# --------------------------------------------------------------- planning --
+def plan_devices(gpus: int, env: dict, visible: int) -> dict:
+    """How this invocation maps onto devices (pure: unit-tested on CPU).
 
-    h = orc.Oracle().taps_lpf(2.4e6, 100e3, 101, 1)
-    blocks = [fm_planar(65540, seed=900 + i) for i in range(4)]
-    if orc.available_reference():
-        ref = orc.Reference()
-        kind = "reference"
+    torch.distributed.run sets WORLD_SIZE: one device per process (LOCAL_RANK),
+    gloo for the timing barrier/reduction.  Otherwise one process drives
+    `gpus` devices with one host thread each."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world > 1:
+        if gpus != world:
+            raise SystemExit(f"--gpus {gpus} but WORLD_SIZE {world}: launch with --nproc-per-node {gpus}")
+        local = int(env.get("LOCAL_RANK", "0"))
+        if local >= visible:
+            raise SystemExit(f"LOCAL_RANK {local} but only {visible} device(s) visible")
+        return {"mode": "ranks", "rank": int(env.get("RANK", "0")), "world": world, "devices": [local]}
+    if gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if env.get("SDR_BENCH_DEVICES"):
+        # rehearsal hook: an explicit device list (e.g. "0,0" drives the
+        # threaded N = 2 path on a one-GPU box); n_gpus then counts threads
+        devs = [int(x) for x in env["SDR_BENCH_DEVICES"].split(",")]
+        if len(devs) != gpus or any(d < 0 or d >= visible for d in devs):
+            raise SystemExit(f"SDR_BENCH_DEVICES={env['SDR_BENCH_DEVICES']} does not name {gpus} visible devices")
+        return {"mode": "threads", "rank": 0, "world": 1, "devices": devs}
+    if gpus > visible:
+        raise SystemExit(f"--gpus {gpus} but only {visible} device(s) visible")
+    return {"mode": "threads", "rank": 0, "world": 1, "devices": list(range(gpus))}
 
-        def make_runner():
-            r = ref.frontend_runner(h, 100)
-            return lambda I, Q: r.run(10, I, Q)
-    else:
-        o = orc.Oracle()
-        kind = "port"
 
-        def make_runner():
-            si, sq, pv = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
-            return lambda I, Q: o.frontend(10, I, Q, h, si, sq, pv)
+def aggregate(per_device_ms: list, units_per_device: int, steps: int) -> dict:
+    """Whole-job throughput over a common start: all devices' units / the
+    slowest device's elapsed time (pure: unit-tested on CPU)."""
+    ms = max(per_device_ms)
+    total = units_per_device * steps * len(per_device_ms)
+    return {"ms": ms, "ms_per_step": ms / steps, "value": total / (ms * 1e-3) / 1e6,
+            "per_gpu_value": [units_per_device * steps / (m * 1e-3) / 1e6 for m in per_device_ms]}
 
-    def measure(nthreads: int, budget: float):
-        counts = [0] * nthreads
-        stop = time.perf_counter() + budget
 
-        def work(t):
-            run = make_runner()
-            i = t
-            while time.perf_counter() < stop:
-                I, Q = blocks[i % len(blocks)]
-                run(I, Q)
-                counts[t] += len(I)
-                i += 1
+# ----------------------------------------------------------- CPU baseline --
+def cpu_baseline(seconds: float, config: str):
+    """The reference's own code timed on this host's cores by
+    the native timer oracle/cpu_bench.cpp: (i) the front end of this config's
+    workload (65,540-pair mode-0 blocks) on 1 thread and on every core of the
+    affinity set, one independent stream per std::thread; (ii) BASELINE
+    config 1 -- the reference program `project 0 mono` on 51,200-pair blocks
+    -- as 1 process and as one process per core.  The reference build
+    (oracle/_ref, kind 'reference') when present, else the C restatement
+    (kind 'port', front end only)."""
+    ref = os.path.join(REPO, "oracle", "_ref", "cpu_bench")
+    port = os.path.join(REPO, "oracle", "cpu_bench_port")
+    exe, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
+    if not os.path.exists(exe):
+        return None
+    cores = int(subprocess.run([exe, "cores"], capture_output=True, text=True, check=True).stdout)
+    block = 65540
 
-        t0 = time.perf_counter()
-        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthreads)]
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        return sum(counts) / (time.perf_counter() - t0) / 1e6, sum(counts)
+    def run(*a):
+        out = subprocess.run([exe, *map(str, a)], capture_output=True, text=True, check=True, timeout=600).stdout
+        return json.loads(out)
 
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
-    one, n1 = measure(1, seconds / 3)
-    many, nm = measure(threads, 2 * seconds / 3)
-    import platform
-
+    one = run("frontend", block, seconds / 4, 1)
+    many = run("frontend", block, seconds / 2, 0)
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -150,283 +178,416 @@ def cpu_baseline(seconds: float):
                     break
     except OSError:
         pass
-    return {"value": round(many, 2), "unit": "MS/s", "cores": threads, "kind": kind,
-            "value_1core": round(one, 2),
-            "sample": f"{nm + n1} IQ pairs in 65,540-pair mode-0 blocks (101-tap FIR+dec10 on I and Q, then the "
-                      f"discriminator), {threads} threads x independent streams for {2 * seconds / 3:.0f} s + 1 "
-                      f"thread for {seconds / 3:.0f} s; host {model} ({platform.machine()}), "
-                      f"{ncpu} cores visible"}
+    rate = lambda d: d["pairs"] / d["seconds"] / 1e6  # noqa: E731
+    res = {"value": round(rate(many), 2), "unit": "MS/s", "cores": many["threads"], "kind": kind,
+           "value_1core": round(rate(one), 2),
+           "sample": f"{one['pairs'] + many['pairs']} IQ pairs in {block:,}-pair mode-0 blocks (101-tap FIR+dec10 "
+                     f"on I and Q, then the discriminator: src/project.cpp:86-90), one independent stream per "
+                     f"std::thread on all {many['threads']} cores of the affinity set for {seconds / 2:.0f} s, and 1 "
+                     f"thread for {seconds / 4:.0f} s; host {model}"}
+    proj = os.path.join(REPO, "oracle", "_ref", "project_ref")
+    if kind == "reference" and os.path.exists(proj):
+        # config 1: ~1 s of the single-process program, then one process per core
+        p1 = run("program", proj, 1500, 1)
+        blocks = max(50, int(1500 * min(1.0, (seconds / 4) / max(p1["seconds"], 1e-3))))
+        pn = run("program", proj, blocks, 0)
+        res["cfg1"] = {
+            "workload": "BASELINE config 1: the reference program `project 0 mono` (src/project.cpp), u8 IQ on "
+                        "stdin in 51,200-pair blocks -> s16 PCM on stdout, wall clock",
+            "value_1proc": round(rate(p1), 2), "value": round(rate(pn), 2), "unit": "MS/s",
+            "procs": pn["procs"], "blocks_per_proc": [1500, blocks],
+            "pcm_ok": p1["pcm_bytes"] == 1500 * 1024 * 2 and pn["pcm_bytes"] == pn["procs"] * blocks * 1024 * 2}
+    return res
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ------------------------------------------------------------ device jobs --
+class Job:
+    """One device's share of the workload: its sdr context, HIP stream,
+    resident synthetic inputs and the step launcher."""
 
-    import sdrhip
+    def __init__(self, cfg_name: str, device: int, seed: int, args):
+        import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        import sdrhip
 
-    cfg = CONFIGS[args.config]
-    ctx = sdrhip.Context(local)
-    # one dedicated (non-null) HIP stream shared by torch and the library, so
-    # torch.cuda.Event timestamps bracket exactly the kernels we launch
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    ctx.set_stream(stream.cuda_stream)
-    ctx.set_arith(sdrhip.ARITH_FMA if args.arith == "fma" else sdrhip.ARITH_EXACT)
-
-    S, n, T = cfg["streams"], cfg["n"], cfg["ntaps"]
-    seed = 1234 + 7919 * rank
-    # taps: the product's coefficient design (C ABI sdr_taps_lpf, bit-identical
-    # to the reference's impulseResponseLPF); setup, not timed
-    if cfg["kind"] == "resample":
-        taps = sdrhip.taps_lpf(240e3 * 147, 16e3, T, 147)
-    else:
-        taps = sdrhip.taps_lpf(2.4e6, 100e3, T, 1)
-    if cfg["kind"] in ("mono_u8", "stereo_u8"):  # src/project.cpp:263-273: audio LPF (+ BPFs) of mode 0
-        d_ha = torch.from_numpy(sdrhip.taps_lpf(240e3, 16e3, 101, 1)).to(dev)
-        d_hp = torch.from_numpy(sdrhip.taps_bpf(240e3, 18.5e3, 19.5e3, 101, 1)).to(dev)
-        d_hs = torch.from_numpy(sdrhip.taps_bpf(240e3, 22e3, 54e3, 101, 1)).to(dev)
-    d_h = torch.from_numpy(taps).to(dev)
-
-    # synthetic input generated on the device (no host traffic), then kept resident
-    iq = torch.empty(S * 2 * n, dtype=torch.uint8, device=dev)
-    ctx.synth_fm_u8_dev(iq, n, S, 2 * n, seed)
-    kind = cfg["kind"]
-    if kind in ("frontend_f32", "fir_block", "fir_block_f16", "resample"):
-        I = torch.empty(S * n, dtype=torch.float32, device=dev)
-        Q = torch.empty(S * n, dtype=torch.float32, device=dev)
-        ctx.u8_to_planar_dev(iq, n, S, 2 * n, I, Q, n)
-        torch.cuda.synchronize(dev)
-        del iq
-    ns = {"resample": 150, "fir_block": T - 1, "fir_block_f16": T - 1}.get(kind, 100)
-    st0 = torch.zeros(S * ns, dtype=torch.float32, device=dev)
-    st1 = torch.zeros(S * ns, dtype=torch.float32, device=dev)
-    p0 = torch.zeros(S, dtype=torch.float32, device=dev)
-    p1 = torch.zeros(S, dtype=torch.float32, device=dev)
-
-    if kind == "mono_u8":
-        D, up, down = cfg["D"], cfg["up"], cfg["down"]
-        na = sdrhip.resample_out_len(up, down, n // D)
-        sd = torch.zeros(S * 50, dtype=torch.float32, device=dev)
-        sa = torch.zeros(S * 100, dtype=torch.float32, device=dev)
-        pcm = torch.empty(S * na, dtype=torch.int16, device=dev)
-        step = lambda: ctx.mono_pcm_u8_dev(D, iq, n, S, 2 * n, d_h, T, st0, st1, ns, p0, p1, sd, 50, up, down,  # noqa
-                                           d_ha, 101, sa, 100, pcm, na)
-        units = S * n
-        bytes_per_pair = 2.0 + 2.0 * na / n  # u8 IQ in, s16 PCM out (intermediates are algorithmically free)
-        flops_per_unit = 2 * 2 * T / D + 10 + 2.0 * 101 / (D * down) + 1
-        unit = "MS/s"
-        metric = "IQ MSamples/sec through the mode-0 mono path (u8 IQ -> s16 PCM)"
-        bound = "valu"
-    elif kind == "stereo_u8":
-        D, up, down = cfg["D"], cfg["up"], cfg["down"]
-        na = sdrhip.resample_out_len(up, down, n // D)
-        z = lambda k: torch.zeros(S * k, dtype=torch.float32, device=dev)  # noqa: E731
-        sbuf = dict(delay=z(50), audio=z(100), slp=z(100), pilot=z(100), stereo=z(100),
-                    pll=torch.tensor([1, 0, 0, 0, 0, 1], dtype=torch.float32, device=dev).repeat(S))
-        taps_s = sdrhip.StereoTaps(d_h.data_ptr(), T, d_ha.data_ptr(), 101, d_hp.data_ptr(), d_hs.data_ptr(), 101)
-        state_s = sdrhip.StereoState(st0.data_ptr(), st1.data_ptr(), ns, p0.data_ptr(), p1.data_ptr(),
-                                     sbuf["delay"].data_ptr(), 50, sbuf["audio"].data_ptr(), sbuf["slp"].data_ptr(),
-                                     100, sbuf["pilot"].data_ptr(), sbuf["stereo"].data_ptr(), 100,
-                                     sbuf["pll"].data_ptr())
-        pcm = torch.empty(S * 2 * na, dtype=torch.int16, device=dev)
-        step = lambda: ctx.stereo_pcm_u8_dev(D, iq, n, S, 2 * n, up, down, 240e3, taps_s, state_s, pcm,  # noqa
-                                             2 * na)
-        units = S * n
-        bytes_per_pair = 2.0 + 4.0 * na / n
-        # front end + mono LPF + 2 BPFs + stereo LPF (2 FLOP per tap) + demod/PLL/mixer
-        flops_per_unit = 2 * 2 * T / D + 10 + (2.0 * 101 * 2 / (D * down) + 2 * 2.0 * 101 / D) + 1
-        unit = "MS/s"
-        metric = "IQ MSamples/sec through the mode-0 stereo path (u8 IQ -> interleaved s16 L/R PCM)"
-        bound = "valu"
-    elif kind in ("frontend_f32", "frontend_u8"):
-        D = cfg["D"]
-        nout = n // D
-        out = torch.empty(S * nout, dtype=torch.float32, device=dev)
-        if kind == "frontend_f32":
-            step = lambda: ctx.frontend_dev(D, I, Q, n, S, n, d_h, T, st0, st1, ns, p0, p1, out, nout)  # noqa: E731
-            bytes_per_pair = 8.0 + 4.0 / D
+        self.torch, self.sdrhip = torch, sdrhip
+        cfg = CONFIGS[cfg_name]
+        self.cfg = cfg
+        torch.cuda.set_device(device)
+        dev = self.dev = torch.device("cuda", device)
+        ctx = self.ctx = sdrhip.Context(device)
+        # one dedicated (non-null) HIP stream shared by torch and the library, so
+        # events bracket exactly the kernels we launch and the stream can be captured
+        self.stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(self.stream)
+        ctx.set_stream(self.stream.cuda_stream)
+        ctx.set_arith(sdrhip.ARITH_FMA if args.arith == "fma" else sdrhip.ARITH_EXACT)
+        self.args = args
+        S, n, T = cfg["streams"], cfg["n"], cfg["ntaps"]
+        kind = self.kind = cfg["kind"]
+        nb = max(1, args.batches)
+        # taps: the product's coefficient design (C ABI sdr_taps_lpf, bit-identical
+        # to the reference's impulseResponseLPF); setup, not timed
+        if kind == "resample":
+            taps = sdrhip.taps_lpf(240e3 * 147, 16e3, T, 147)
         else:
-            step = lambda: ctx.frontend_u8_dev(D, iq, n, S, 2 * n, d_h, T, st0, st1, ns, p0, p1, out, nout)  # noqa
-            bytes_per_pair = 2.0 + 4.0 / D
-        units = S * n  # IQ pairs per step
-        flops_per_unit = 2 * 2 * T / D + 10
-        unit = "MS/s"
-        metric = "IQ MSamples/sec through FIR+decimate+FM-demod"
-        # f32 planar input: 8.4 B against ~41 FLOP per pair -> HBM-bound; the u8
-        # wire format moves 2.4 B per pair, which puts the exact (no-FMA) FIR
-        # arithmetic above the ridge -> VALU-bound
-        bound = "hbm" if kind == "frontend_f32" else "valu"
-    elif kind == "resample":
-        up, down = cfg["up"], cfg["down"]
-        ny = sdrhip.resample_out_len(up, down, n)
-        out = torch.empty(S * ny, dtype=torch.float32, device=dev)
-        step = lambda: ctx.resample_dev(up, down, I, n, S, n, d_h, T, st0, ns, out, ny)  # noqa: E731
-        units = S * n  # input samples per step
-        bytes_per_pair = 4.0 + 4.0 * up / down
-        flops_per_unit = 2.0 * (T / up) * up / down
-        unit = "MS/s"
-        metric = "IF MSamples/sec (input) through the polyphase resampler"
-        bound = "hbm"
-    elif kind == "fir_block":  # I and Q as two streams
-        out = torch.empty(S * n, dtype=torch.float32, device=dev)
-        IQ = torch.stack([I[:n], Q[:n]])
-        step = lambda: ctx.fir_block_dev(IQ, n, 2, n, d_h, T, st0, ns, out, n)  # noqa: E731
-        units = n  # IQ pairs per step (I and Q each n samples)
-        bytes_per_pair = 16.0
-        flops_per_unit = 2.0 * 2 * T
-        unit = "MS/s"
-        metric = "IQ MSamples/sec through a 1024-tap FIR"
-        bound = "valu"
-    else:  # fir_block_f16: fp16 storage of I and Q (converted once, untimed)
-        IQ = torch.stack([I[:n], Q[:n]])
-        IQh = torch.empty(2 * n, dtype=torch.float16, device=dev)
-        ctx.f32_to_f16_dev(IQ, 2 * n, IQh)
-        sth = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
-        out = torch.empty(2 * n, dtype=torch.float32, device=dev)
-        step = lambda: ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, sth, ns, out, n)  # noqa: E731
-        units = n
-        bytes_per_pair = 2.0 * 2 + 8.0  # fp16 in, fp32 out
-        flops_per_unit = 2.0 * 2 * T
-        unit = "MS/s"
-        metric = "IQ MSamples/sec through a 1024-tap FIR"
-        bound = "valu"
-        # error of this arm against the exact fp32 path on the same first block
-        ref = torch.empty(2 * n, dtype=torch.float32, device=dev)
-        z32 = torch.zeros(2 * ns, dtype=torch.float32, device=dev)
-        ctx.fir_block_dev(IQ, n, 2, n, d_h, T, z32, ns, ref, n)
-        z16 = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
-        got = torch.empty(2 * n, dtype=torch.float32, device=dev)
-        ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, z16, ns, got, n)
-        torch.cuda.synchronize(dev)
-        err = float((got - ref).abs().max())
-        scale = float(d_h.abs().sum()) * float(IQ.abs().max())
-        tolerance = {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale,
-                     "norm": "sum|h| * max|x|", "rms_err": float((got - ref).pow(2).mean().sqrt())}
+            taps = sdrhip.taps_lpf(2.4e6, 100e3, T, 1)
+        if kind in ("mono_u8", "stereo_u8"):  # src/project.cpp:263-273: audio LPF (+ BPFs) of mode 0
+            d_ha = torch.from_numpy(sdrhip.taps_lpf(240e3, 16e3, 101, 1)).to(dev)
+            d_hp = torch.from_numpy(sdrhip.taps_bpf(240e3, 18.5e3, 19.5e3, 101, 1)).to(dev)
+            d_hs = torch.from_numpy(sdrhip.taps_bpf(240e3, 22e3, 54e3, 101, 1)).to(dev)
+        d_h = self.d_h = torch.from_numpy(taps).to(dev)
 
-    # W warmup steps, then more of the same launches until >= --warm-seconds
-    # of wall time has passed: an idle MI355X sits at ~0.1 GHz and its clock
-    # ramps over tens of ms; a few warmup steps (<1 ms) would time part of
-    # the ramp, not the sustained rate a streaming receiver runs at.
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    t_warm = time.perf_counter()
-    while time.perf_counter() - t_warm < args.warm_seconds:
-        for _ in range(10):
-            step()
-        torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    t_wall = time.perf_counter()
-    e0.record(stream)
-    for _ in range(args.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t_wall
-    if world > 1:
-        dist.barrier()
-    ms_gpu = e0.elapsed_time(e1)
-    ms = torch.tensor([ms_gpu, wall * 1e3], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-    ms_events, ms_wall = float(ms[0]), float(ms[1])
+        # synthetic input generated on the device (no host traffic), kept resident;
+        # nb distinct batches (different seeds)
+        iqs = []
+        for b in range(nb):
+            iq = torch.empty(S * 2 * n, dtype=torch.uint8, device=dev)
+            ctx.synth_fm_u8_dev(iq, n, S, 2 * n, seed + 104729 * b)
+            iqs.append(iq)
+        planar = []
+        if kind in ("frontend_f32", "fir_block", "fir_block_f16", "resample"):
+            for iq in iqs:
+                I = torch.empty(S * n, dtype=torch.float32, device=dev)
+                Q = torch.empty(S * n, dtype=torch.float32, device=dev)
+                ctx.u8_to_planar_dev(iq, n, S, 2 * n, I, Q, n)
+                planar.append((I, Q))
+            torch.cuda.synchronize(dev)
+            iqs = []
+        ns = {"resample": 150, "fir_block": T - 1, "fir_block_f16": T - 1}.get(kind, 100)
+        st0 = torch.zeros(S * ns, dtype=torch.float32, device=dev)
+        st1 = torch.zeros(S * ns, dtype=torch.float32, device=dev)
+        p0 = torch.zeros(S, dtype=torch.float32, device=dev)
+        p1 = torch.zeros(S, dtype=torch.float32, device=dev)
+        self.keep = [st0, st1, p0, p1, planar, iqs]
+        self.tolerance = None
+        steps = []
 
-    ms_per_step = ms_events / args.steps
-    total_units = units * args.steps * world
-    value = total_units / (ms_events * 1e-3) / 1e6
+        if kind == "mono_u8":
+            D, up, down = cfg["D"], cfg["up"], cfg["down"]
+            na = sdrhip.resample_out_len(up, down, n // D)
+            sd = torch.zeros(S * 50, dtype=torch.float32, device=dev)
+            sa = torch.zeros(S * 100, dtype=torch.float32, device=dev)
+            pcm = torch.empty(S * na, dtype=torch.int16, device=dev)
+            self.keep += [sd, sa, pcm, d_ha]
+            for iq in iqs:
+                steps.append(lambda iq=iq: ctx.mono_pcm_u8_dev(D, iq, n, S, 2 * n, d_h, T, st0, st1, ns, p0, p1, sd,
+                                                               50, up, down, d_ha, 101, sa, 100, pcm, na))
+            self.units = S * n
+            self.bytes_per_pair = 2.0 + 2.0 * na / n  # u8 IQ in, s16 PCM out (intermediates are algorithmically free)
+            # FIR MACs at 2 FLOP each (front end, audio LPF at the IF rate / 5) + the discriminator
+            self.flops_per_unit = 2 * 2 * T / D + 2.0 * 101 / (D * down) + 1.0 / D
+            self.metric = "IQ MSamples/sec through the mode-0 mono path (u8 IQ -> s16 PCM)"
+            self.bound = "valu"
+        elif kind == "stereo_u8":
+            D, up, down = cfg["D"], cfg["up"], cfg["down"]
+            na = sdrhip.resample_out_len(up, down, n // D)
+            z = lambda k: torch.zeros(S * k, dtype=torch.float32, device=dev)  # noqa: E731
+            sbuf = dict(delay=z(50), audio=z(100), slp=z(100), pilot=z(100), stereo=z(100),
+                        pll=torch.tensor([1, 0, 0, 0, 0, 1], dtype=torch.float32, device=dev).repeat(S))
+            taps_s = sdrhip.StereoTaps(d_h.data_ptr(), T, d_ha.data_ptr(), 101, d_hp.data_ptr(), d_hs.data_ptr(), 101)
+            state_s = sdrhip.StereoState(st0.data_ptr(), st1.data_ptr(), ns, p0.data_ptr(), p1.data_ptr(),
+                                         sbuf["delay"].data_ptr(), 50, sbuf["audio"].data_ptr(),
+                                         sbuf["slp"].data_ptr(), 100, sbuf["pilot"].data_ptr(),
+                                         sbuf["stereo"].data_ptr(), 100, sbuf["pll"].data_ptr())
+            pcm = torch.empty(S * 2 * na, dtype=torch.int16, device=dev)
+            self.keep += [sbuf, taps_s, state_s, pcm, d_ha, d_hp, d_hs]
+            for iq in iqs:
+                steps.append(lambda iq=iq: ctx.stereo_pcm_u8_dev(D, iq, n, S, 2 * n, up, down, 240e3, taps_s,
+                                                                 state_s, pcm, 2 * na))
+            self.units = S * n
+            self.bytes_per_pair = 2.0 + 4.0 * na / n
+            # front end + mono and stereo audio LPFs (IF/5 rate) + pilot and stereo BPFs (IF rate)
+            self.flops_per_unit = 2 * 2 * T / D + 2 * 2.0 * 101 / (D * down) + 2 * 2.0 * 101 / D + 1.0 / D
+            self.metric = "IQ MSamples/sec through the mode-0 stereo path (u8 IQ -> interleaved s16 L/R PCM)"
+            self.bound = "valu"
+        elif kind in ("frontend_f32", "frontend_u8"):
+            D = cfg["D"]
+            nout = n // D
+            out = torch.empty(S * nout, dtype=torch.float32, device=dev)
+            self.keep.append(out)
+            if kind == "frontend_f32":
+                for I, Q in planar:
+                    steps.append(lambda I=I, Q=Q: ctx.frontend_dev(D, I, Q, n, S, n, d_h, T, st0, st1, ns, p0, p1,
+                                                                   out, nout))
+                self.bytes_per_pair = 8.0 + 4.0 / D
+            else:
+                for iq in iqs:
+                    steps.append(lambda iq=iq: ctx.frontend_u8_dev(D, iq, n, S, 2 * n, d_h, T, st0, st1, ns, p0, p1,
+                                                                   out, nout))
+                self.bytes_per_pair = 2.0 + 4.0 / D
+            self.units = S * n  # IQ pairs per step
+            # 2 channels x T/D MACs x 2 FLOP, + the discriminator (~10 FLOP per decimated output)
+            self.flops_per_unit = 2 * 2 * T / D + 10.0 / D
+            self.metric = "IQ MSamples/sec through FIR+decimate+FM-demod"
+            # f32 planar input: 8.4 B against ~41 FLOP per pair -> HBM-bound; the u8
+            # wire format moves 2.4 B per pair, which puts the exact (no-FMA) FIR
+            # arithmetic above the ridge -> VALU-bound (DESIGN.md 4.1)
+            self.bound = "hbm" if kind == "frontend_f32" else "valu"
+        elif kind == "resample":
+            up, down = cfg["up"], cfg["down"]
+            ny = sdrhip.resample_out_len(up, down, n)
+            out = torch.empty(S * ny, dtype=torch.float32, device=dev)
+            self.keep.append(out)
+            for I, _ in planar:
+                steps.append(lambda I=I: ctx.resample_dev(up, down, I, n, S, n, d_h, T, st0, ns, out, ny))
+            self.units = S * n  # input samples per step
+            self.bytes_per_pair = 4.0 + 4.0 * up / down
+            self.flops_per_unit = 2.0 * (T / up) * up / down
+            self.metric = "IF MSamples/sec (input) through the polyphase resampler"
+            self.bound = "hbm"
+        elif kind == "fir_block":  # I and Q as two streams
+            out = torch.empty(S * n, dtype=torch.float32, device=dev)
+            IQs = [torch.stack([I[:n], Q[:n]]) for I, Q in planar]
+            self.keep += [out, IQs]
+            for IQ in IQs:
+                steps.append(lambda IQ=IQ: ctx.fir_block_dev(IQ, n, 2, n, d_h, T, st0, ns, out, n))
+            self.units = n  # IQ pairs per step (I and Q each n samples)
+            self.bytes_per_pair = 16.0
+            self.flops_per_unit = 2.0 * 2 * T
+            self.metric = "IQ MSamples/sec through a 1024-tap FIR"
+            self.bound = "valu"
+        else:  # fir_block_f16: fp16 storage of I and Q (converted once, untimed)
+            IQhs = []
+            for I, Q in planar:
+                IQ = torch.stack([I[:n], Q[:n]])
+                IQh = torch.empty(2 * n, dtype=torch.float16, device=dev)
+                ctx.f32_to_f16_dev(IQ, 2 * n, IQh)
+                IQhs.append(IQh)
+            sth = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
+            out = torch.empty(2 * n, dtype=torch.float32, device=dev)
+            self.keep += [IQhs, sth, out]
+            for IQh in IQhs:
+                steps.append(lambda IQh=IQh: ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, sth, ns, out, n))
+            self.units = n
+            self.bytes_per_pair = 2.0 * 2 + 8.0  # fp16 in, fp32 out
+            self.flops_per_unit = 2.0 * 2 * T
+            self.metric = "IQ MSamples/sec through a 1024-tap FIR"
+            self.bound = "valu"
+            # error of this arm against the exact fp32 path on the same first block
+            I, Q = planar[0]
+            IQ = torch.stack([I[:n], Q[:n]])
+            ref = torch.empty(2 * n, dtype=torch.float32, device=dev)
+            z32 = torch.zeros(2 * ns, dtype=torch.float32, device=dev)
+            ctx.fir_block_dev(IQ, n, 2, n, d_h, T, z32, ns, ref, n)
+            z16 = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
+            got = torch.empty(2 * n, dtype=torch.float32, device=dev)
+            ctx.fir_block_f16_dev(IQhs[0], n, 2, n, d_h, T, z16, ns, got, n)
+            torch.cuda.synchronize(dev)
+            err = float((got - ref).abs().max())
+            scale = float(d_h.abs().sum()) * float(IQ.abs().max())
+            self.tolerance = {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale,
+                              "norm": "sum|h| * max|x|", "rms_err": float((got - ref).pow(2).mean().sqrt())}
+        self.steps = steps
+        self.graph = None
+        torch.cuda.synchronize(dev)
+
+    # -- launching
+    def launch(self, k: int):
+        """Enqueue k steps (cycling over the input batches); graphs when captured."""
+        i = 0
+        if self.graph is not None:
+            g, gs = self.graph
+            while k - i >= gs:
+                g.launch()
+                i += gs
+        for j in range(i, k):
+            self.steps[(self._next + j) % len(self.steps)]()
+        self._next = (self._next + k) % len(self.steps)
+
+    _next = 0
+
+    def capture(self, gs: int):
+        """Record gs consecutive steps into a HIP graph (gs a multiple of the batch
+        count keeps the batch rotation aligned across replays)."""
+        if self.graph is not None:
+            self.graph[0].close()
+        nb = len(self.steps)
+        gs = max(nb, gs - gs % nb)
+        self._next = 0
+        self.graph = (self.ctx.capture(lambda: [self.steps[j % nb]() for j in range(gs)]), gs)
+
+    def warm(self, warmup: int, seconds: float):
+        """W warmup steps, then more of the same launches until >= seconds of
+        wall time has passed: an idle MI355X sits at ~0.1 GHz and its clock
+        ramps over tens of ms; a few warmup steps (<1 ms) would time part of
+        the ramp, not the sustained rate a streaming receiver runs at."""
+        torch = self.torch
+        self.launch(warmup)
+        torch.cuda.synchronize(self.dev)
+        t = time.perf_counter()
+        while time.perf_counter() - t < seconds:
+            self.launch(10)
+            torch.cuda.synchronize(self.dev)
+
+    def timed(self, k: int, barrier=None):
+        """Exactly k steps between HIP events on this device's stream; returns (ms_events, wall_s)."""
+        torch = self.torch
+        torch.cuda.synchronize(self.dev)
+        if barrier is not None:
+            barrier()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t = time.perf_counter()
+        e0.record(self.stream)
+        self.launch(k)
+        e1.record(self.stream)
+        torch.cuda.synchronize(self.dev)
+        wall = time.perf_counter() - t
+        if barrier is not None:
+            barrier()
+        return e0.elapsed_time(e1), wall
+
+    def close(self):
+        if self.graph is not None:
+            self.graph[0].close()
+            self.graph = None
+        self.torch.cuda.synchronize(self.dev)
+        self.ctx.close()
+
+
+def run_device(cfg_name, device, seed, args, barrier=None, side=True):
+    """Setup + warmup + the timed region on one device (a host thread or a rank)."""
+    job = Job(cfg_name, device, seed, args)
+    res = {"device": device}
+    try:
+        if not args.no_graph:
+            job.capture(args.graph_steps)
+        job.warm(args.warmup, args.warm_seconds)
+        res["ms"], res["wall"] = job.timed(args.steps, barrier)
+        # Side measurement (fused front end, exact run only): the same launches
+        # under SDR_ARITH_FMA -- one fused multiply-add per tap, not the
+        # reference's bits (tolerance-tested, DESIGN.md 2); never `value`.
+        if side and args.arith == "exact" and job.kind in ("frontend_f32", "frontend_u8") \
+                and not args.no_fma_variant:
+            job.ctx.set_arith(job.sdrhip.ARITH_FMA)
+            if not args.no_graph:
+                job.capture(args.graph_steps)
+            job.warm(max(args.warmup, 2), args.warm_seconds)
+            res["fma_ms"], _ = job.timed(args.steps)
+            job.ctx.set_arith(job.sdrhip.ARITH_EXACT)
+        res["job"] = {k: getattr(job, k) for k in ("units", "bytes_per_pair", "flops_per_unit", "metric", "bound",
+                                                  "kind", "tolerance")}
+    finally:
+        job.close()
+    return res
+
+
+def roofline(job: dict, ms_per_step: float, config: str) -> dict:
     launch_s = ms_per_step * 1e-3
-    if bound == "hbm":
-        achieved = units * bytes_per_pair / launch_s / 1e9
+    units = job["units"]
+    if job["bound"] == "hbm":
+        achieved = units * job["bytes_per_pair"] / launch_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4)}
     else:
-        achieved = units * flops_per_unit / launch_s / 1e12
+        achieved = units * job["flops_per_unit"] / launch_s / 1e12
         # fp16 arm: v_dot2_f32_f16 retires two products per lane per issue -> twice the fp32 vector peak
-        peak = FP32_VALU_PEAK_TFLOPS * (2 if kind == "fir_block_f16" else 1)
+        peak = FP32_VALU_PEAK_TFLOPS * (2 if job["kind"] == "fir_block_f16" else 1)
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4)}
     traffic = None
-    tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    tpath = os.path.join(REPO, "profiles", f"traffic_{config}.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
-            t = json.load(f)
-        traffic = t.get("hbm_bytes_per_launch")
+            traffic = json.load(f).get("hbm_bytes_per_launch")
         roof["traffic_source"] = os.path.relpath(tpath, REPO)
     roof["traffic"] = traffic
-    roof["algorithmic_bytes_per_launch"] = int(units * bytes_per_pair)
+    roof["algorithmic_bytes_per_launch"] = int(units * job["bytes_per_pair"])
+    return roof
 
-    if kind != "fir_block_f16":
-        tolerance = None
-    # Side measurement (1 GPU, fused front end, exact run only): the same
-    # launches under SDR_ARITH_FMA -- one fused multiply-add per tap, not the
-    # reference's bits (tolerance-tested).  Reported beside the
-    # headline, never as `value`.
+
+def main(argv=None):
+    args = parse(argv)
+    import torch
+
+    plan = plan_devices(args.gpus, os.environ, torch.cuda.device_count())
+    cfg = CONFIGS[args.config]
+    results = []
+    if plan["mode"] == "threads":
+        devs = plan["devices"]
+        bar = threading.Barrier(len(devs))
+        errors = []
+
+        def worker(i, d):
+            try:
+                results.append(run_device(args.config, d, 1234 + 7919 * i, args,
+                                          barrier=bar.wait if len(devs) > 1 else None, side=len(devs) == 1))
+            except BaseException as e:  # noqa: BLE001 -- reported below, after every thread ended
+                errors.append((d, e))
+                bar.abort()
+
+        ths = [threading.Thread(target=worker, args=(i, d)) for i, d in enumerate(devs)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if errors:
+            d, e = errors[0]
+            raise RuntimeError(f"device {d} failed") from e
+        results.sort(key=lambda r: r["device"])  # stable: rehearsal lists may repeat a device
+        rank, world = 0, len(devs)
+        per_ms = [r["ms"] for r in results]
+        distinct = len(set(devs))
+        wall = max(r["wall"] for r in results)
+    else:
+        import torch.distributed as dist
+
+        rank, world = plan["rank"], plan["world"]
+        # CPU (gloo) group: the timing barrier and max-over-ranks only; the data
+        # path has no collective at all
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            r = run_device(args.config, plan["devices"][0], 1234 + 7919 * rank, args, barrier=dist.barrier,
+                           side=False)
+            t = torch.tensor([r["ms"], r["wall"]], dtype=torch.float64)
+            allt = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(allt, t)
+        finally:
+            dist.destroy_process_group()
+        results = [r]
+        distinct = world
+        per_ms = [float(x[0]) for x in allt]
+        wall = max(float(x[1]) for x in allt)
+
+    job = results[0]["job"]
+    agg = aggregate(per_ms, job["units"], args.steps)
+    roof = roofline(job, agg["ms_per_step"], args.config)
     fma_variant = None
-    if world == 1 and args.arith == "exact" and kind in ("frontend_f32", "frontend_u8") and not args.no_fma_variant:
-        ctx.set_arith(sdrhip.ARITH_FMA)
-        for _ in range(max(args.warmup, 2)):
-            step()
-        torch.cuda.synchronize(dev)
-        t_warm = time.perf_counter()
-        while time.perf_counter() - t_warm < args.warm_seconds:
-            for _ in range(10):
-                step()
-            torch.cuda.synchronize(dev)
-        f0 = torch.cuda.Event(enable_timing=True)
-        f1 = torch.cuda.Event(enable_timing=True)
-        f0.record(stream)
-        for _ in range(args.steps):
-            step()
-        f1.record(stream)
-        torch.cuda.synchronize(dev)
-        ctx.set_arith(sdrhip.ARITH_EXACT)
-        fms = f0.elapsed_time(f1) / args.steps
-        fval = units / (fms * 1e-3) / 1e6
-        if bound == "hbm":
-            ffrac = units * bytes_per_pair / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS
-        else:
-            ffrac = units * flops_per_unit / (fms * 1e-3) / 1e12 / FP32_VALU_PEAK_TFLOPS
+    if len(results) == 1 and "fma_ms" in results[0]:
+        fms = results[0]["fma_ms"] / args.steps
+        fval = job["units"] / (fms * 1e-3) / 1e6
         fma_variant = {"arith": "fma (SDR_ARITH_FMA): one fused multiply-add per tap; within the fp32 tolerance, "
                                 "not the reference's bits",
-                       "value": round(fval, 1), "ms_per_step": round(fms, 4), "roofline_frac": round(ffrac, 4)}
+                       "value": round(fval, 1), "ms_per_step": round(fms, 4),
+                       "roofline_frac": roofline(job, fms, args.config)["frac"]}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("cfg2", "cfg2u8", "cfg4"):
-        cpu = cpu_baseline(args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("cfg2", "cfg2u8", "cfg4", "cfg4x8"):
+        cpu = cpu_baseline(args.cpu_seconds, args.config)
     if rank == 0:
+        kind = job["kind"]
         line = {
-            "metric": metric, "value": round(value, 1), "unit": unit, "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f16" if kind == "fir_block_f16" else "f32",
-            "data": "synthetic",
-            "config": {"workload": cfg["workload"], "streams_per_gpu": S, "pairs_per_stream_per_step": n,
-                       "ntaps": T, "parallelism": f"{world} GPU(s) x independent streams, no data-path collective",
+            "metric": job["metric"], "value": round(agg["value"], 1), "unit": "MS/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["ms_per_step"], 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f16" if kind == "fir_block_f16" else "f32", "data": "synthetic",
+            "config": {"workload": cfg["workload"], "streams_per_gpu": cfg["streams"],
+                       "pairs_per_stream_per_step": cfg["n"], "ntaps": cfg["ntaps"],
+                       "parallelism": f"{world} GPU(s) x independent streams, no data-path collective "
+                                      f"({'one host thread per device' if plan['mode'] == 'threads' else 'one process per device, gloo timing barrier'})",
+                       "devices_opened": distinct, "input_batches": max(1, args.batches),
+                       "launch": "direct" if args.no_graph else f"HIP graph of {args.graph_steps} steps",
                        "state_carried_across_steps": True,
                        "arith": ("fma: one fused multiply-add per tap, tolerance-tested (DESIGN.md 2)"
                                  if args.arith == "fma" else "exact: the reference's bits")},
+            "per_gpu": {"value": [round(v, 1) for v in agg["per_gpu_value"]],
+                        "ms_per_step": [round(m / args.steps, 4) for m in per_ms]},
             "roofline": roof, "cpu_baseline": cpu,
-            **({"tolerance": tolerance} if tolerance else {}),
+            **({"tolerance": job["tolerance"]} if job["tolerance"] else {}),
             **({"fma_variant": fma_variant} if fma_variant else {}),
-            "wall_ms": round(ms_wall, 3),
+            "wall_ms": round(wall * 1e3, 3),
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -98,6 +98,20 @@ int sdr_event_record(sdr_ctx *ctx, sdr_event *ev);      /* marks the work enqueu
 int sdr_event_synchronize(sdr_ctx *ctx, sdr_event *ev); /* blocks until that work is done */
 int sdr_event_destroy(sdr_ctx *ctx, sdr_event *ev);
 
+/* HIP-graph capture of the context's stream: sdr_graph_begin, then any
+ * stream-ordered *_dev / *_async calls (recorded, not run), then
+ * sdr_graph_end instantiates them; sdr_graph_launch replays the recorded
+ * sequence on the context's stream with the same pointers (state arrays
+ * carry across replays exactly as across direct calls).  Replaces the
+ * per-block launch sequence of a streaming caller (src/project.cpp:289-318
+ * runs one block at a time) by one launch.  The stream must not be the null
+ * stream; calls that synchronise fail while capturing. */
+typedef struct sdr_graph sdr_graph;
+int sdr_graph_begin(sdr_ctx *ctx);
+int sdr_graph_end(sdr_ctx *ctx, sdr_graph **graph);
+int sdr_graph_launch(sdr_ctx *ctx, sdr_graph *graph);
+int sdr_graph_destroy(sdr_ctx *ctx, sdr_graph *graph);
+
 /* --------------------------------------------------- coefficient design -- */
 /* impulseResponseLPF / impulseResponseBPF, src/filter.cpp:14-49
  * (filter.h:17, :27): windowed-sinc taps with the up-factor gain folded in,

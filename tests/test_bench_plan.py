@@ -1,0 +1,97 @@
+"""bench.py's multi-GPU planning and aggregation (CPU): `--gpus N` drives N
+devices from one process (one host thread each), torch.distributed.run
+launches one device per rank, and the whole-job rate is all devices' units
+over the slowest device's time (independent streams, no
+collective)."""
+import importlib.util
+import os
+import threading
+
+import pytest
+
+from conftest import REPO
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_plan_threads_opens_every_device():
+    b = _bench()
+    p = b.plan_devices(8, {}, visible=8)
+    assert p == {"mode": "threads", "rank": 0, "world": 1, "devices": list(range(8))}
+    assert b.plan_devices(1, {}, visible=8)["devices"] == [0]
+    with pytest.raises(SystemExit):
+        b.plan_devices(4, {}, visible=2)  # never silently measure fewer GPUs than asked
+    with pytest.raises(SystemExit):
+        b.plan_devices(0, {}, visible=2)
+    # rehearsal hook: two host threads on one device
+    assert b.plan_devices(2, {"SDR_BENCH_DEVICES": "0,0"}, visible=1)["devices"] == [0, 0]
+    with pytest.raises(SystemExit):
+        b.plan_devices(3, {"SDR_BENCH_DEVICES": "0,0"}, visible=1)
+
+
+def test_plan_ranks_one_device_each():
+    b = _bench()
+    env = {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2"}
+    assert b.plan_devices(4, env, visible=8) == {"mode": "ranks", "rank": 2, "world": 4, "devices": [2]}
+    with pytest.raises(SystemExit):
+        b.plan_devices(8, env, visible=8)  # --gpus must match the launcher's world size
+
+
+def test_aggregate_is_all_units_over_the_slowest_device():
+    b = _bench()
+    units, steps = 1024 * 65540, 100
+    agg = b.aggregate([10.0, 10.5, 9.8, 10.2], units, steps)
+    assert agg["ms"] == 10.5
+    assert agg["value"] == pytest.approx(4 * units * steps / 10.5e-3 / 1e6)
+    assert agg["per_gpu_value"][2] == pytest.approx(units * steps / 9.8e-3 / 1e6)
+    # weak scaling: N equal devices give N times one device
+    one = b.aggregate([10.0], units, steps)["value"]
+    assert b.aggregate([10.0] * 8, units, steps)["value"] == pytest.approx(8 * one)
+
+
+def test_thread_driver_collects_every_device(monkeypatch):
+    """main()'s thread mode with a fake per-device runner: every device is run
+    in its own thread behind one barrier and reported."""
+    b = _bench()
+    seen = []
+    lock = threading.Lock()
+
+    def fake_run_device(cfg, device, seed, args, barrier=None, side=True):
+        if barrier is not None:
+            barrier()
+        with lock:
+            seen.append((device, threading.get_ident(), side))
+        job = {"units": 1000, "bytes_per_pair": 8.4, "flops_per_unit": 41.4, "metric": "m", "bound": "hbm",
+               "kind": "frontend_f32", "tolerance": None}
+        return {"device": device, "ms": 1.0 + device, "wall": 0.01, "job": job}
+
+    monkeypatch.setattr(b, "run_device", fake_run_device)
+
+    class FakeCuda:
+        @staticmethod
+        def device_count():
+            return 4
+
+    class FakeTorch:
+        cuda = FakeCuda
+
+    import sys
+
+    monkeypatch.setitem(sys.modules, "torch", FakeTorch)
+    lines = []
+    monkeypatch.setattr("builtins.print", lambda s, **k: lines.append(s))
+    b.main(["--gpus", "4", "--steps", "10", "--no-cpu-baseline"])
+    import json
+
+    out = json.loads(lines[-1])
+    assert sorted(d for d, _, _ in seen) == [0, 1, 2, 3]
+    assert len({t for _, t, _ in seen}) == 4  # one host thread per device
+    assert not any(side for _, _, side in seen)  # no side measurement at N > 1
+    assert out["n_gpus"] == 4 and out["config"]["devices_opened"] == 4
+    assert out["ms_per_step"] == pytest.approx(0.4)  # the slowest device: 4 ms / 10 steps
+    assert len(out["per_gpu"]["value"]) == 4

@@ -1,0 +1,205 @@
+"""GPU parity at BASELINE.json's full sizes, through the exact launches the
+benchmark times (f32 planar `frontend_dev`, state carried across steps):
+
+* config 2: 1,024 streams x 65,540 pairs, two consecutive steps -- sampled
+  streams against the oracle bit for bit, and EVERY stream's carried state
+  (state_i/q = the block's last 100 inputs; prev_i/q = its last decimated
+  I/Q, recomputed in numpy in the reference's fp32 order) bit for bit;
+* config 2 under SDR_ARITH_FMA: every stream within the SURVEY 8(d) bar of
+  the exact path;
+* config 4: 262,150-pair blocks (2 consecutive, 3 streams), and one stream
+  as a single 8,388,800-pair call (the bench's cfg4x8 per-stream call)
+  against the oracle run block by block -- block-size independence,
+  src/filter.cpp:139;
+* config 5: the 1024-tap FIR over 2 x 1,048,576 samples, windows at the
+  start (real state), middle and end checked against the oracle (each
+  window's state is the preceding 1,023 inputs, src/filter.cpp:82).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_bits, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _z(k):
+    return np.zeros(k, np.float32)
+
+
+def _dev(sdrhip, ctx, a):
+    return sdrhip.DeviceArray.from_numpy(ctx, np.ascontiguousarray(a))
+
+
+def _last_output(h, x, D):
+    """Last decimated output of every row of x (y[nout-1] = sum_k h[k] x[n-D-k]),
+    accumulated k = 0..T-1 from 0.0f with separately rounded products and sums
+    (numpy float32 ops never fuse) -- src/filter.cpp:131-135."""
+    n = x.shape[1]
+    acc = np.zeros(x.shape[0], np.float32)
+    for k in range(len(h)):
+        acc = acc + np.float32(h[k]) * x[:, n - D - k]
+    return acc
+
+
+def _planar_batch(sdrhip, ctx, nstreams, n, seed):
+    d_iq = sdrhip.DeviceArray(ctx, nstreams * 2 * n)
+    ctx.synth_fm_u8_dev(d_iq, n, nstreams, 2 * n, seed=seed)
+    d_I = sdrhip.DeviceArray(ctx, nstreams * n * 4)
+    d_Q = sdrhip.DeviceArray(ctx, nstreams * n * 4)
+    ctx.u8_to_planar_dev(d_iq, n, nstreams, 2 * n, d_I, d_Q, n)
+    d_iq.free()
+    return d_I, d_Q
+
+
+def test_cfg2_full_f32_two_steps(gpu_ctx, oracle, built_lib):
+    sdrhip = built_lib
+    S, n, D = 1024, 65540, 10
+    nout = n // D
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_si, d_sq = _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32)), _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32))
+    d_pi, d_pq = _dev(sdrhip, gpu_ctx, _z(S)), _dev(sdrhip, gpu_ctx, _z(S))
+    d_out = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
+    sample = (0, 1, 2, 255, 511, 700, 1022, 1023)
+    ors = {s: dict(si=_z(100), sq=_z(100), prev=_z(2)) for s in sample}
+    for step, seed in enumerate((301, 302)):
+        d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, seed)
+        gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
+        gpu_ctx.synchronize()
+        got = d_out.download().reshape(S, nout)
+        I = d_I.download().reshape(S, n)
+        Q = d_Q.download().reshape(S, n)
+        for s in sample:
+            want = oracle.frontend(D, I[s], Q[s], h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"])
+            assert_bits(got[s], want, f"step {step} stream {s}")
+        # every stream's carried state
+        assert_bits(d_si.download().reshape(S, 100), I[:, n - 100:], f"step {step} state_i (all streams)")
+        assert_bits(d_sq.download().reshape(S, 100), Q[:, n - 100:], f"step {step} state_q (all streams)")
+        assert_bits(d_pi.download(), _last_output(h, I, D), f"step {step} prev_i (all streams)")
+        assert_bits(d_pq.download(), _last_output(h, Q, D), f"step {step} prev_q (all streams)")
+        assert np.isfinite(got).all()
+        d_I.free()
+        d_Q.free()
+
+
+def test_cfg2_full_fma_tolerance(gpu_ctx, built_lib):
+    """SDR_ARITH_FMA at full size: every stream's demod within 1e-5 of the exact
+    path where the decimated envelope I^2+Q^2 >= 1e-3; state exact."""
+    sdrhip = built_lib
+    S, n, D = 1024, 65540, 10
+    nout = n // D
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, 303)
+    outs, states = {}, {}
+    for mode in (sdrhip.ARITH_EXACT, sdrhip.ARITH_FMA):
+        gpu_ctx.set_arith(mode)
+        try:
+            d_si, d_sq = _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32)), _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32))
+            d_pi, d_pq = _dev(sdrhip, gpu_ctx, _z(S)), _dev(sdrhip, gpu_ctx, _z(S))
+            d_out = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
+            gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
+            gpu_ctx.synchronize()
+        finally:
+            gpu_ctx.set_arith(sdrhip.ARITH_EXACT)
+        outs[mode] = d_out.download().reshape(S, nout)
+        states[mode] = (d_si.download(), d_sq.download(), d_pi.download(), d_pq.download())
+    # the decimated I/Q envelope, exact (unfused FIR calls)
+    d_yi = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
+    d_yq = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
+    for d_x, d_y in ((d_I, d_yi), (d_Q, d_yq)):
+        d_s = _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32))
+        gpu_ctx.fir_decim_dev(D, d_x, n, S, n, d_h, 101, d_s, 100, d_y, nout)
+    gpu_ctx.synchronize()
+    yi = d_yi.download().reshape(S, nout).astype(np.float64)
+    yq = d_yq.download().reshape(S, nout).astype(np.float64)
+    ok = (yi * yi + yq * yq) >= 1e-3
+    diff = np.abs(outs[sdrhip.ARITH_FMA].astype(np.float64) - outs[sdrhip.ARITH_EXACT])
+    assert ok.mean() > 0.99
+    assert diff[ok].max() <= 1e-5, f"FMA demod off by {diff[ok].max():.3g}"
+    assert not np.array_equal(outs[sdrhip.ARITH_FMA], outs[sdrhip.ARITH_EXACT])  # it did run the FMA kernel
+    for a, b in zip(states[sdrhip.ARITH_FMA][:2], states[sdrhip.ARITH_EXACT][:2]):
+        assert_bits(a, b, "FMA state (raw inputs: exact by construction)")
+    bound = 4e-6 * float(np.abs(h).sum()) * 1.0
+    for a, b in zip(states[sdrhip.ARITH_FMA][2:], states[sdrhip.ARITH_EXACT][2:]):
+        assert np.abs(a.astype(np.float64) - b).max() <= bound
+
+
+def test_cfg4_blocks_vs_oracle(gpu_ctx, oracle, built_lib):
+    """3 streams x 2 consecutive 262,150-pair blocks, batched f32 call, bitwise
+    with all carried state."""
+    sdrhip = built_lib
+    S, n, D = 3, 262150, 10
+    nout = n // D
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_si, d_sq = _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32)), _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32))
+    d_pi, d_pq = _dev(sdrhip, gpu_ctx, _z(S)), _dev(sdrhip, gpu_ctx, _z(S))
+    d_out = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
+    ors = [dict(si=_z(100), sq=_z(100), prev=_z(2)) for _ in range(S)]
+    for b, seed in enumerate((41, 42)):
+        d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, seed)
+        gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
+        gpu_ctx.synchronize()
+        got = d_out.download().reshape(S, nout)
+        I, Q = d_I.download().reshape(S, n), d_Q.download().reshape(S, n)
+        for s in range(S):
+            want = oracle.frontend(D, I[s], Q[s], h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"])
+            assert_bits(got[s], want, f"block {b} stream {s}")
+        assert_bits(d_si.download().reshape(S, 100), np.stack([o["si"] for o in ors]), "state_i")
+        assert_bits(d_sq.download().reshape(S, 100), np.stack([o["sq"] for o in ors]), "state_q")
+        assert_bits(d_pi.download(), np.array([o["prev"][0] for o in ors], np.float32), "prev_i")
+        assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), "prev_q")
+
+
+def test_cfg4_single_call_equals_blocks(gpu_ctx, oracle, built_lib):
+    """One stream as ONE 8,388,800-pair call (32 x 262,150) == the oracle run
+    block by block over the same samples, outputs and state bitwise."""
+    sdrhip = built_lib
+    nblk, blk, D = 32, 262150, 10
+    n = nblk * blk
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, 1, n, 4242)
+    st0 = np.random.default_rng(3).uniform(-0.7, 0.7, (2, 100)).astype(np.float32)  # a non-zero carried state
+    pv0 = np.array([0.25, -0.5], np.float32)
+    d_si, d_sq = _dev(sdrhip, gpu_ctx, st0[0]), _dev(sdrhip, gpu_ctx, st0[1])
+    d_pi, d_pq = _dev(sdrhip, gpu_ctx, pv0[:1]), _dev(sdrhip, gpu_ctx, pv0[1:])
+    d_out = sdrhip.DeviceArray(gpu_ctx, n // D * 4)
+    gpu_ctx.frontend_dev(D, d_I, d_Q, n, 1, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, n // D)
+    gpu_ctx.synchronize()
+    got = d_out.download()
+    I, Q = d_I.download(), d_Q.download()
+    si, sq, pv = st0[0].copy(), st0[1].copy(), pv0.copy()
+    want = np.concatenate([oracle.frontend(D, I[b * blk:(b + 1) * blk], Q[b * blk:(b + 1) * blk], h, si, sq, pv)
+                           for b in range(nblk)])
+    assert_bits(got, want, "one call vs 32 oracle blocks")
+    assert_bits(d_si.download(), si, "state_i")
+    assert_bits(d_sq.download(), sq, "state_q")
+    assert_bits(np.concatenate([d_pi.download(), d_pq.download()]), pv, "prev")
+
+
+def test_cfg5_full_windows(gpu_ctx, oracle, built_lib):
+    """BASELINE config 5 at full size: 2 x 1,048,576 samples through the exact
+    1024-tap FIR; windows checked against the oracle (any window equals a
+    block-by-block run whose state is the 1,023 inputs before it)."""
+    sdrhip = built_lib
+    n, T, W = 1048576, 1024, 4096
+    h = oracle.taps_lpf(2.4e6, 100e3, T, 1)
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, 1, n, 55)
+    x = np.stack([d_I.download(), d_Q.download()])
+    st0 = np.random.default_rng(4).uniform(-0.7, 0.7, (2, T - 1)).astype(np.float32)
+    d_x, d_st = _dev(sdrhip, gpu_ctx, x), _dev(sdrhip, gpu_ctx, st0)
+    d_y = sdrhip.DeviceArray(gpu_ctx, 2 * n * 4)
+    gpu_ctx.fir_block_dev(d_x, n, 2, n, d_h, T, d_st, T - 1, d_y, n)
+    gpu_ctx.synchronize()
+    y = d_y.download().reshape(2, n)
+    for c in range(2):
+        want0 = oracle.fir_block(x[c, :W], h, st0[c].copy())
+        assert_bits(y[c, :W], want0, f"channel {c} first window")
+        for a in (n // 2 + 13, n - W):
+            want = oracle.fir_block(x[c, a:a + W], h, x[c, a - (T - 1):a].copy())
+            assert_bits(y[c, a:a + W], want, f"channel {c} window at {a}")
+    assert_bits(d_st.download().reshape(2, T - 1), x[:, n - (T - 1):], "state")
