@@ -39,14 +39,6 @@
 #pragma clang fp contract(off)
 
 // Build switches (same-box A/B with scripts/build_ab_tree.sh):
-// SDR_EDGE_DRAIN: retire edge-tile loads inside the edge path;
-// SDR_PREV_SCALAR: read the carried prev_I/prev_Q with scalar loads.
-#ifndef SDR_EDGE_DRAIN
-#define SDR_EDGE_DRAIN 1
-#endif
-#ifndef SDR_PREV_SCALAR
-#define SDR_PREV_SCALAR 1
-#endif
 // SDR_FIR_NT / SDR_FIR_NT_U8: streamed span loads with the non-temporal
 // hint (read once from HBM; the neighbour's halo re-read still hits L2).
 // Measured (warm, same box): f32 -1..5 %, u8 wire +6 % -> f32 only.
@@ -161,7 +153,7 @@ __device__ __forceinline__ float edge_at(const float* x, const uint8_t* iq, int 
 struct TileRef {
   int s;              // stream
   int t;              // tile within the stream
-  long long m_start;  // first output the tile computes (includes the wave overlap)
+  long long m_start;  // first output the tile computes (t*ADV; tiles t >= 1 recompute their first E)
   long long pb;       // stream position of LDS index 0
   const float* x0;
   const float* x1;
@@ -176,7 +168,13 @@ __device__ __forceinline__ TileRef tile_ref(const FirLaunch& a, int lin) {
   TileRef r;
   r.s = lin / a.tiles_per_stream;
   r.t = lin - r.s * a.tiles_per_stream;
-  r.m_start = (long long)r.t * G::ADV - G::E;
+  // Tile t computes outputs [t*ADV, t*ADV + NW*64*R).  Its first E outputs
+  // (lane 0 of each wave) are the previous wave's last E, recomputed so no
+  // wave waits for another; tile 0 has no predecessor: its lane 0 outputs
+  // are the stream's first and are stored, with the carried prev_*.  So
+  // tiles_per_stream = ceil((nout - E) / ADV): at cfg2 (6,554 outputs,
+  // ADV 126, E 2) exactly 52 tiles, none partial.
+  r.m_start = (long long)r.t * G::ADV;
   r.pb = (long long)D * r.m_start - G::HALO;
   r.st0 = a.state0 + (long long)r.s * a.ns;
   r.st1 = NCH == 2 ? a.state1 + (long long)r.s * a.ns : nullptr;
@@ -304,13 +302,11 @@ __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long 
       }
     }
   }
-#if SDR_EDGE_DRAIN
   // Retire the edge loads inside the (rare) edge path.  Left pending, they
   // make hipcc's waitcnt pass merge the edge and interior paths
   // conservatively and drain the whole vector-memory queue (vmcnt(0)) at
   // every tile's scan -- the next tiles' prefetch included.
   __builtin_amdgcn_s_waitcnt(0);
-#endif
 }
 
 template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
@@ -417,7 +413,6 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // end of the iteration (tile 0 only).
     float old_pi = 0.0f, old_pq = 0.0f;
     if constexpr (DEMOD) {
-#if SDR_PREV_SCALAR
       // scalar loads (lgkmcnt, not vmcnt): a conditional vector load here
       // makes the waitcnt pass drain the prefetch queue at the scan.  The
       // value is the launch's input: only this workgroup rewrites it, after
@@ -428,12 +423,6 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
         old_pi = ((cf)a.prev0)[s];
         old_pq = ((cf)a.prev1)[s];
       }
-#else
-      if (tr.t == 0 && tid == 1) {
-        old_pi = a.prev0[tr.s];
-        old_pq = a.prev1[tr.s];
-      }
-#endif
     }
 
     // ---- 1. registers -> LDS (after every read of the previous tile), then
@@ -586,11 +575,13 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     if constexpr (DEMOD) {
       // ---- 3. discriminator in registers.  The decimated sample before
       // output r=0 is lane-1's last output (a wave shuffle); lane 0's
-      // outputs are the wave's overlap and are not stored; at the start of
-      // the stream (tile 0, wave 0, lane 1 -> output 0) it is the carried prev_*.
+      // outputs are the wave's overlap and are not stored, except at the
+      // start of the stream (tile 0, wave 0, lane 0 -> outputs 0..R-1),
+      // whose predecessor is the carried prev_*.
       float pI = __shfl_up(acc0[R - 1], 1, 64);
       float pQ = __shfl_up(acc1[R - 1], 1, 64);
-      if (tr.t == 0 && tid == 1) {
+      const bool first = tr.t == 0 && tid == 0;
+      if (first) {
         pI = old_pi;
         pQ = old_pq;
       }
@@ -606,7 +597,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
       // ablate 3 (timing only): no output stores unless the result is a
       // value it never is, so the scan still runs
-      if (lane >= 1 && (a.ablate != 3 || d[0] == 12345.0f)) {
+      if ((lane >= 1 || first) && (a.ablate != 3 || d[0] == 12345.0f)) {
         if (vec && m0 + R <= nout) {
           if constexpr (R == 2) {
             if constexpr (SDR_OUT_NT && SRC == Src::F32) {
@@ -674,23 +665,23 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           }
         }
       }
-#if SDR_EDGE_DRAIN
       __builtin_amdgcn_s_waitcnt(0);  // as in edge_fill: keep the waitcnt pass from draining at the next scan
-#endif
       __syncthreads();
       if constexpr (DEMOD) {
         // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
         // recomputed in the reference's order from the staged strip:
         // input D*(nout-1) - k = n - D - k sits at strip index STRIP - D - k
-        if (tid == 0) {
-          float yi = 0.0f, yq = 0.0f;
-          for (int k = 0; k < T; ++k) {
-            const float hk = h[k];
-            yi = yi + hk * strip0[G::STRIP - D - k];
-            yq = yq + hk * strip1[G::STRIP - D - k];
-          }
-          a.prev0[tr.s] = yi;
-          a.prev1[tr.s] = yq;
+        // (lane c < 2 runs channel c; groups of 8 LDS reads in flight -- a
+        // full unroll would hold all T reads live and cost a wave per SIMD
+        // of occupancy for the whole kernel)
+        if (tid < 2) {
+          using hconst = const __attribute__((address_space(4))) float*;
+          const hconst hc = (hconst)h;
+          const float* sp = (tid == 0 ? strip0 : strip1) + (G::STRIP - D);
+          float y = 0.0f;
+#pragma unroll 8
+          for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
+          (tid == 0 ? a.prev0 : a.prev1)[tr.s] = y;
         }
       }
       // state <- last ns input samples (src/filter.cpp:139)
@@ -790,7 +781,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
   const long long nout = a.n / D;
-  a.tiles_per_stream = (int)((nout + G::ADV - 1) / G::ADV);
+  a.tiles_per_stream = nout > G::E ? (int)((nout - G::E + G::ADV - 1) / G::ADV) : 1;
   const long long total = (long long)a.tiles_per_stream * a.nstreams;
   if (total <= 0 || total > 0x7fffffffLL) return hipErrorInvalidValue;
   const int ncu = device_cu_count();
@@ -845,7 +836,7 @@ bool geometry_ok(int D, int T, int ns, bool demod, Variant v) {
   const int halo = (T - 1 + 3) / 4 * 4;
   const int E = demod ? v.R : 0;
   const long long adv = (long long)v.NW * (64 * v.R - E);
-  return (long long)D * (adv - E) - halo >= 0;
+  return (long long)D * adv - halo >= 0;
 }
 
 template <int NCH, bool DEMOD, Src SRC>

@@ -150,7 +150,9 @@ def cpu_baseline(seconds: float, config: str):
     """The reference's own code timed on this host's cores by
     the native timer oracle/cpu_bench.cpp: (i) the front end of this config's
     workload (65,540-pair mode-0 blocks) on 1 thread and on every core of the
-    affinity set, one independent stream per std::thread; (ii) BASELINE
+    process's CPU share (the affinity set capped by the cgroup CPU quota and
+    OMP_NUM_THREADS: a GPU box grants 16 of its 256 cores), one independent
+    stream per std::thread; (ii) BASELINE
     config 1 -- the reference program `project 0 mono` on 51,200-pair blocks
     -- as 1 process and as one process per core.  The reference build
     (oracle/_ref, kind 'reference') when present, else the C restatement
@@ -183,8 +185,11 @@ def cpu_baseline(seconds: float, config: str):
            "value_1core": round(rate(one), 2),
            "sample": f"{one['pairs'] + many['pairs']} IQ pairs in {block:,}-pair mode-0 blocks (101-tap FIR+dec10 "
                      f"on I and Q, then the discriminator: src/project.cpp:86-90), one independent stream per "
-                     f"std::thread on all {many['threads']} cores of the affinity set for {seconds / 2:.0f} s, and 1 "
-                     f"thread for {seconds / 4:.0f} s; host {model}"}
+                     f"std::thread on all {many['threads']} cores of this process's CPU share for {seconds / 2:.0f} s, "
+                     f"and 1 thread for {seconds / 4:.0f} s; host {model}",
+           "cpu_share": {"cores": many["threads"], "affinity": many["affinity"],
+                         "cgroup_quota": many["cgroup_quota"] or None,
+                         "omp_num_threads": many["omp_num_threads"] or None}}
     proj = os.path.join(REPO, "oracle", "_ref", "project_ref")
     if kind == "reference" and os.path.exists(proj):
         # config 1: ~1 s of the single-process program, then one process per core
@@ -451,9 +456,13 @@ def run_device(cfg_name, device, seed, args, barrier=None, side=True):
     job = Job(cfg_name, device, seed, args)
     res = {"device": device}
     try:
+        # the first launches run directly: they size the library's scratch
+        # (allocations cannot happen inside a capture); then record the graph
+        job.launch(args.warmup)
+        job.torch.cuda.synchronize(job.dev)
         if not args.no_graph:
             job.capture(args.graph_steps)
-        job.warm(args.warmup, args.warm_seconds)
+        job.warm(0, args.warm_seconds)
         res["ms"], res["wall"] = job.timed(args.steps, barrier)
         # Side measurement (fused front end, exact run only): the same launches
         # under SDR_ARITH_FMA -- one fused multiply-add per tap, not the
@@ -461,9 +470,13 @@ def run_device(cfg_name, device, seed, args, barrier=None, side=True):
         if side and args.arith == "exact" and job.kind in ("frontend_f32", "frontend_u8") \
                 and not args.no_fma_variant:
             job.ctx.set_arith(job.sdrhip.ARITH_FMA)
+            job.graph[0].close() if job.graph else None
+            job.graph = None
+            job.launch(max(args.warmup, 2))
+            job.torch.cuda.synchronize(job.dev)
             if not args.no_graph:
                 job.capture(args.graph_steps)
-            job.warm(max(args.warmup, 2), args.warm_seconds)
+            job.warm(0, args.warm_seconds)
             res["fma_ms"], _ = job.timed(args.steps)
             job.ctx.set_arith(job.sdrhip.ARITH_EXACT)
         res["job"] = {k: getattr(job, k) for k in ("units", "bytes_per_pair", "flops_per_unit", "metric", "bound",

@@ -10,7 +10,8 @@
 //   cpu_bench frontend <block_pairs> <seconds> <threads>
 //       the mode-0 front end (src/project.cpp:86-90: FIR+dec10 on I and Q,
 //       then fmDemodArctan) on independent synthetic streams, one stream per
-//       std::thread, each thread pinned to its own core of the affinity set.
+//       std::thread, one per core of the CPU share (<threads> = 0), each pinned to
+//       its own core of the affinity set.
 //       Prints {"pairs":..., "seconds":..., "threads":...}.
 //   cpu_bench program <project_binary> <blocks> <procs>
 //       BASELINE config 1: `<project_binary> 0 mono` (the reference program,
@@ -20,7 +21,8 @@
 //       clock from spawn to the last exit.  Prints
 //       {"pairs":..., "seconds":..., "procs":..., "pcm_bytes":...}.
 //   cpu_bench cores
-//       Prints the affinity-set size (sched_getaffinity).
+//       Prints the CPU share: the affinity set (sched_getaffinity) capped by
+//       the cgroup CPU quota and OMP_NUM_THREADS (cpu_share below).
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
 #endif
@@ -95,6 +97,46 @@ std::vector<int> affinity_cpus() {
   return cpus;
 }
 
+// The CPU share this process may use: the affinity set, capped by the
+// cgroup CPU quota (a GPU box's container sees every core of the machine in
+// its affinity set but is granted a fraction of them) and by
+// OMP_NUM_THREADS when the environment sets it to the same share.
+struct Share {
+  size_t affinity;
+  int quota;  // ceil(cgroup quota / period), 0 = unlimited / unknown
+  int omp;    // OMP_NUM_THREADS, 0 = unset
+  int cores;
+};
+
+int read_quota() {
+  long q = -1, per = 0;
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota|max> <period>"
+    char buf[64] = {};
+    if (std::fscanf(f, "%63s %ld", buf, &per) == 2 && std::strcmp(buf, "max") != 0) q = std::atol(buf);
+    std::fclose(f);
+  } else if (FILE* f1 = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // cgroup v1
+    if (std::fscanf(f1, "%ld", &q) != 1) q = -1;
+    std::fclose(f1);
+    if (FILE* f2 = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (std::fscanf(f2, "%ld", &per) != 1) per = 0;
+      std::fclose(f2);
+    }
+  }
+  return (q > 0 && per > 0) ? (int)((q + per - 1) / per) : 0;
+}
+
+Share cpu_share() {
+  Share s;
+  s.affinity = affinity_cpus().size();
+  s.quota = read_quota();
+  const char* e = std::getenv("OMP_NUM_THREADS");
+  s.omp = e ? std::atoi(e) : 0;
+  s.cores = (int)s.affinity;
+  if (s.quota > 0 && s.quota < s.cores) s.cores = s.quota;
+  if (s.omp > 0 && s.omp < s.cores) s.cores = s.omp;
+  return s;
+}
+
 // Synthetic baseband FM at 2.4 MS/s: message 0.8 sin(2pi 1k t)
 // + 0.1 sin(2pi 19k t), 75 kHz deviation, amplitude 0.7, quantised to the
 // wire's u8 levels.  `seed` shifts the phase so streams differ.
@@ -119,7 +161,8 @@ std::vector<unsigned char> synth_u8(long pairs, unsigned seed) {
 
 int run_frontend(long n, double seconds, int threads) {
   const std::vector<int> cpus = affinity_cpus();
-  if (threads <= 0) threads = (int)cpus.size();
+  const Share share = cpu_share();
+  if (threads <= 0) threads = share.cores;
   std::vector<float> h(101);
   ref_taps_lpf(2.4e6f, 100e3f, 101, 1, h.data());
   // 4 blocks per thread (planar float, the filter.h boundary), as
@@ -173,8 +216,9 @@ int run_frontend(long n, double seconds, int threads) {
     total += pairs[t];
     wall = secs[t] > wall ? secs[t] : wall;
   }
-  std::printf("{\"pairs\": %lld, \"seconds\": %.6f, \"threads\": %d, \"cores_visible\": %zu}\n", total, wall, threads,
-              cpus.size());
+  std::printf("{\"pairs\": %lld, \"seconds\": %.6f, \"threads\": %d, \"affinity\": %zu, \"cgroup_quota\": %d, "
+              "\"omp_num_threads\": %d}\n",
+              total, wall, threads, share.affinity, share.quota, share.omp);
   return 0;
 }
 
@@ -243,8 +287,8 @@ int run_program(const char* prog, long blocks, int procs) {
   const double wall = std::chrono::duration<double>(clk::now() - t0).count();
   long long pcm = 0;
   for (auto& k : kids) pcm += k.pcm;
-  std::printf("{\"pairs\": %lld, \"seconds\": %.6f, \"procs\": %d, \"pcm_bytes\": %lld, \"cores_visible\": %zu}\n",
-              (long long)procs * blocks * (block_bytes / 2), wall, procs, pcm, affinity_cpus().size());
+  std::printf("{\"pairs\": %lld, \"seconds\": %.6f, \"procs\": %d, \"pcm_bytes\": %lld}\n",
+              (long long)procs * blocks * (block_bytes / 2), wall, procs, pcm);
   return 0;
 }
 
@@ -252,14 +296,14 @@ int run_program(const char* prog, long blocks, int procs) {
 
 int main(int argc, char** argv) {
   if (argc >= 2 && !std::strcmp(argv[1], "cores")) {
-    std::printf("%zu\n", affinity_cpus().size());
+    std::printf("%d\n", cpu_share().cores);
     return 0;
   }
   if (argc == 5 && !std::strcmp(argv[1], "frontend"))
     return run_frontend(std::atol(argv[2]), std::atof(argv[3]), std::atoi(argv[4]));
   if (argc == 5 && !std::strcmp(argv[1], "program")) {
     int procs = std::atoi(argv[4]);
-    if (procs <= 0) procs = (int)affinity_cpus().size();
+    if (procs <= 0) procs = cpu_share().cores;
     return run_program(argv[2], std::atol(argv[3]), procs);
   }
   std::fprintf(stderr,

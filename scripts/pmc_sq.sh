@@ -1,19 +1,20 @@
 #!/bin/bash
-# SQ/LDS counter passes for the front-end kernel (one pass per group; no
-# tracing domains combined with --pmc).
+# SQ/LDS counter passes for one kernel of one bench config (one pass per
+# group, no tracing domains beside --pmc; <= 8 SQ counters per pass).
+#   TAG=pmc CFG=cfg2 KERNEL=fir_tile [SDR_ABLATE=1] bash scripts/pmc_sq.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 CFG=${CFG:-cfg2}
 i=0
 while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$PWD/$OUT/p$i" -o pmc \
-     -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2>> "$OUT/err.log"
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$PWD/$OUT/p$i" -o pmc \
+     -- python3 bench.py --config $CFG --steps 3 --warmup 1 --warm-seconds 0 --no-cpu-baseline --no-fma-variant \
+        --no-graph > /dev/null 2>> "$OUT/err.log"
   rc=$?; echo "pass $i ($grp) rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done <<GROUPS
 ${GROUPS_OVERRIDE:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS

@@ -42,12 +42,15 @@ def _last_output(h, x, D):
     return acc
 
 
-def _planar_batch(sdrhip, ctx, nstreams, n, seed):
-    d_iq = sdrhip.DeviceArray(ctx, nstreams * 2 * n)
-    ctx.synth_fm_u8_dev(d_iq, n, nstreams, 2 * n, seed=seed)
-    d_I = sdrhip.DeviceArray(ctx, nstreams * n * 4)
-    d_Q = sdrhip.DeviceArray(ctx, nstreams * n * 4)
-    ctx.u8_to_planar_dev(d_iq, n, nstreams, 2 * n, d_I, d_Q, n)
+def _planar_batch(sdrhip, ctx, nstreams, n, seed, stride=None):
+    """Device synthetic FM, planar f32 rows of `stride` (>= n, a multiple of 4)."""
+    stride = stride or n
+    iq_stride = (2 * n + 7) // 8 * 8
+    d_iq = sdrhip.DeviceArray(ctx, nstreams * iq_stride)
+    ctx.synth_fm_u8_dev(d_iq, n, nstreams, iq_stride, seed=seed)
+    d_I = sdrhip.DeviceArray(ctx, nstreams * stride * 4)
+    d_Q = sdrhip.DeviceArray(ctx, nstreams * stride * 4)
+    ctx.u8_to_planar_dev(d_iq, n, nstreams, iq_stride, d_I, d_Q, stride)
     d_iq.free()
     return d_I, d_Q
 
@@ -138,14 +141,16 @@ def test_cfg4_blocks_vs_oracle(gpu_ctx, oracle, built_lib):
     d_pi, d_pq = _dev(sdrhip, gpu_ctx, _z(S)), _dev(sdrhip, gpu_ctx, _z(S))
     d_out = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
     ors = [dict(si=_z(100), sq=_z(100), prev=_z(2)) for _ in range(S)]
+    stride = n + 2  # 262,150 is not a multiple of 4: 16-B aligned rows
     for b, seed in enumerate((41, 42)):
-        d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, seed)
-        gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
+        d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, seed, stride)
+        gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, stride, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
         gpu_ctx.synchronize()
         got = d_out.download().reshape(S, nout)
-        I, Q = d_I.download().reshape(S, n), d_Q.download().reshape(S, n)
+        I, Q = d_I.download().reshape(S, stride)[:, :n], d_Q.download().reshape(S, stride)[:, :n]
         for s in range(S):
-            want = oracle.frontend(D, I[s], Q[s], h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"])
+            want = oracle.frontend(D, np.ascontiguousarray(I[s]), np.ascontiguousarray(Q[s]), h, ors[s]["si"],
+                                   ors[s]["sq"], ors[s]["prev"])
             assert_bits(got[s], want, f"block {b} stream {s}")
         assert_bits(d_si.download().reshape(S, 100), np.stack([o["si"] for o in ors]), "state_i")
         assert_bits(d_sq.download().reshape(S, 100), np.stack([o["sq"] for o in ors]), "state_q")
