@@ -19,16 +19,24 @@ struct sdr_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t cur = nullptr;
+  // the stereo pipeline's fork/join: a second stream for the branches that
+  // do not wait for the PLL recurrence, and the two events that join them
+  // (created on first use)
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   int arith = SDR_ARITH_EXACT;
   // grow-only device scratch for the host-pointer wrappers and internal use
-  void* buf[17] = {};
-  size_t cap[17] = {};
+  void* buf[19] = {};
+  size_t cap[19] = {};
   std::string err;
 };
 
 namespace {
 
-enum Slot { kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp, kPipe0, kPipe1, kPipe2, kPipe3, kPipe4, kPipe5, kPipe6 };
+enum Slot {
+  kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp,
+  kPipe0, kPipe1, kPipe2, kPipe3, kPipe4, kPipe5, kPipe6, kPipe7, kPipe8
+};
 
 int fail(sdr_ctx* c, int code, const char* fmt, ...) {
   if (c) {
@@ -181,7 +189,11 @@ int sdr_ctx_destroy(sdr_ctx* c) {
   (void)hipStreamSynchronize(c->cur);
   for (void* b : c->buf)
     if (b) (void)hipFree(b);
+  if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->own) (void)hipStreamDestroy(c->own);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->fork) (void)hipEventDestroy(c->fork);
+  if (c->join) (void)hipEventDestroy(c->join);
   delete c;
   return SDR_OK;
 }
@@ -685,36 +697,64 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
   if (nstreams > 1 && pcm_stride < 2 * na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
   const long long dstride = (nd + 3) / 4 * 4, astride = (na + 3) / 4 * 4;
   const size_t dbytes = (size_t)nstreams * dstride * sizeof(float), abytes = (size_t)nstreams * astride * sizeof(float);
+  const long long pstride = (nd + 1 + 3) / 4 * 4;  // PLL oscillator arguments (+ the incoming nco_state)
   float* demod = static_cast<float*>(scratch(c, kPipe0, dbytes));
-  float* work = static_cast<float*>(scratch(c, kPipe1, dbytes));  // delayed demod, then the mixer output
+  float* delayed = static_cast<float*>(scratch(c, kPipe1, dbytes));
   float* mono = static_cast<float*>(scratch(c, kPipe2, abytes));
   float* pilot = static_cast<float*>(scratch(c, kPipe3, dbytes));
   float* sband = static_cast<float*>(scratch(c, kPipe4, dbytes));
   float* slp = static_cast<float*>(scratch(c, kPipe5, abytes));
-  if (!demod || !work || !mono || !pilot || !sband || !slp) return fail(c, SDR_ENOMEM, "pipeline buffers");
+  float* args = static_cast<float*>(scratch(c, kPipe6, (size_t)nstreams * pstride * sizeof(float)));
+  float* mixed = static_cast<float*>(scratch(c, kPipe7, dbytes));
+  if (!demod || !delayed || !mono || !pilot || !sband || !slp || !args || !mixed)
+    return fail(c, SDR_ENOMEM, "pipeline buffers");
+  if (!c->side) {
+    SDR_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    SDR_HIP(c, hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+    SDR_HIP(c, hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
+  }
+  // The PLL recurrence (one lane per stream, latency-bound) is the critical
+  // path: front end -> pilot BPF -> recurrence -> NCO x stereo band ->
+  // stereo LPF -> PCM.  The branches that do not wait for it -- delay + mono
+  // resampler (src/project.cpp:114-116) and the stereo band-pass (:121) --
+  // run on a second stream beside it and join before the mixer.  Captured
+  // into a HIP graph, the fork/join becomes two parallel branches.
   // src/project.cpp:72-93: front end
   if ((rc = sdr_frontend_u8_dev(c, D, iq, npairs, nstreams, iq_stride, taps->h_rf, taps->rf_taps, st->state_i,
                                 st->state_q, st->ns_rf, st->prev_i, st->prev_q, demod, dstride)))
     return rc;
-  // :114-116: mono = resample(delay(demod))
-  if ((rc = sdr_delay_f32_dev(c, demod, nd, nstreams, dstride, st->delay_state, st->ns_delay, work, dstride)))
-    return rc;
-  if ((rc = sdr_resample_f32_dev(c, up, down, work, nd, nstreams, dstride, taps->h_audio, taps->audio_taps,
-                                 st->state_audio, st->ns_audio, mono, astride)))
-    return rc;
-  // :120-121: pilot and stereo band-pass filters on the undelayed demod
+  SDR_HIP(c, hipEventRecord(c->fork, c->cur));
+  SDR_HIP(c, hipStreamWaitEvent(c->side, c->fork, 0));
+  {
+    hipStream_t main = c->cur;
+    c->cur = c->side;
+    // :114-116: mono = resample(delay(demod)); :121: stereo band-pass
+    rc = sdr_delay_f32_dev(c, demod, nd, nstreams, dstride, st->delay_state, st->ns_delay, delayed, dstride);
+    if (!rc)
+      rc = sdr_resample_f32_dev(c, up, down, delayed, nd, nstreams, dstride, taps->h_audio, taps->audio_taps,
+                                st->state_audio, st->ns_audio, mono, astride);
+    if (!rc)
+      rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_stereo, taps->bpf_taps, st->stereo_state,
+                                 st->ns_bpf, sband, dstride);
+    hipError_t e = rc ? hipSuccess : hipEventRecord(c->join, c->side);
+    c->cur = main;
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  }
+  // :120: pilot band-pass, then the PLL recurrence (:123-126: 19 kHz, ncoScale 2,
+  // phaseAdjust 0, bandwidth 0.01)
   if ((rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_pilot, taps->bpf_taps, st->pilot_state,
                                   st->ns_bpf, pilot, dstride)))
     return rc;
-  if ((rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_stereo, taps->bpf_taps,
-                                  st->stereo_state, st->ns_bpf, sband, dstride)))
-    return rc;
-  // :123-126: PLL on the pilot (19 kHz, ncoScale 2, phaseAdjust 0, bandwidth 0.01) fused with the mixer
-  if ((rc = sdr_fm_pll_dev(c, pilot, nd, nstreams, dstride, 19e3f, audio_fs, 2.0f, 0.0f, 0.01f, st->pll, sband,
-                           dstride, work, dstride)))
-    return rc;
+  hipError_t e = sdr::launch_pll_recurrence(pilot, nd, nstreams, dstride, 19e3f, audio_fs, 2.0f, 0.0f, 0.01f, st->pll,
+                                            args, pstride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "pll launch");
+  // join: the NCO mixed with the stereo band (pointwiseMultiply x2, :127)
+  SDR_HIP(c, hipStreamWaitEvent(c->cur, c->join, 0));
+  e = sdr::launch_nco(args, pstride, nd, nstreams, 2.0f, 0.0f, sband, dstride, mixed, dstride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "nco launch");
   // :129: the stereo channel through the same audio resampler, its own state
-  if ((rc = sdr_resample_f32_dev(c, up, down, work, nd, nstreams, dstride, taps->h_audio, taps->audio_taps,
+  if ((rc = sdr_resample_f32_dev(c, up, down, mixed, nd, nstreams, dstride, taps->h_audio, taps->audio_taps,
                                  st->stereo_lp_state, st->ns_audio, slp, astride)))
     return rc;
   // :131-132 + 304-314: L/R, interleave, s16

@@ -86,6 +86,14 @@ hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_s
                       float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
                       long long mix_stride, float* out, long long out_stride, float* args, long long args_stride,
                       hipStream_t st);
+// the two halves of launch_pll: the per-stream recurrence (records each
+// sample's oscillator argument in args) and the parallel NCO (+ mixer)
+hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
+                                 float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
+                                 long long args_stride, hipStream_t st);
+hipError_t launch_nco(const float* args, long long args_stride, long long n, int nstreams, float nco_scale,
+                      float phase_adjust, const float* mix, long long mix_stride, float* out, long long out_stride,
+                      hipStream_t st);
 hipError_t launch_stereo_pcm(const float* a, const float* b, long long n, int nstreams, long long stride,
                              int16_t* pcm, long long pcm_stride, hipStream_t st);
 hipError_t launch_synth_fm_u8(uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

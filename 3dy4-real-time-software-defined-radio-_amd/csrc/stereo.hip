@@ -133,17 +133,30 @@ __global__ __launch_bounds__(kWG) void stereo_pcm_kernel(const float* __restrict
 
 }  // namespace
 
+hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
+                                 float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
+                                 long long args_stride, hipStream_t st) {
+  hipLaunchKernelGGL(pll_kernel, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams, in_stride,
+                     freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_nco(const float* args, long long args_stride, long long n, int nstreams, float nco_scale,
+                      float phase_adjust, const float* mix, long long mix_stride, float* out, long long out_stride,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(nco_kernel, dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0, st, args,
+                     args_stride, n, nco_scale, phase_adjust, mix, mix_stride, out, out_stride);
+  return hipGetLastError();
+}
+
 hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
                       float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
                       long long mix_stride, float* out, long long out_stride, float* args, long long args_stride,
                       hipStream_t st) {
-  hipLaunchKernelGGL(pll_kernel, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams, in_stride,
-                     freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
-  hipError_t e = hipGetLastError();
+  hipError_t e = launch_pll_recurrence(in, n, nstreams, in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll,
+                                       args, args_stride, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(nco_kernel, dim3((unsigned)((n + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0, st, args,
-                     args_stride, n, nco_scale, phase_adjust, mix, mix_stride, out, out_stride);
-  return hipGetLastError();
+  return launch_nco(args, args_stride, n, nstreams, nco_scale, phase_adjust, mix, mix_stride, out, out_stride, st);
 }
 
 hipError_t launch_stereo_pcm(const float* a, const float* b, long long n, int nstreams, long long stride,

@@ -175,6 +175,30 @@ int main(int argc, char* argv[]) {
     check(sdr_event_create(g_ctx, &done[i]), "event_create");
   }
 
+  // One block's device work: copy in, the whole mono/stereo path, copy out
+  // (~10 launches).  For one stream these are latency-bound, so after the
+  // first block each ring slot's sequence is captured once into a HIP graph
+  // and replayed: one launch per block (SDR_PROJECT_NO_GRAPH=1 launches them
+  // one by one).
+  auto enqueue = [&](int k) {
+    check(sdr_copy_h2d_async(g_ctx, d_in[k], h_in[k], block_size), "copy_h2d_async");
+    const uint8_t* iq = static_cast<const uint8_t*>(d_in[k]);
+    int16_t* pcm = static_cast<int16_t*>(d_out[k]);
+    if (mono)
+      check(sdr_mono_pcm_u8_dev(g_ctx, rf_decim, iq, npairs, 1, 2 * npairs, taps.h_rf, num_taps, st.state_i,
+                                st.state_q, st.ns_rf, st.prev_i, st.prev_q, st.delay_state, st.ns_delay, audio_up,
+                                audio_decim, taps.h_audio, audio_taps, st.state_audio, st.ns_audio, pcm, pcm_len),
+            "mono_pcm_u8_dev");
+    else
+      check(sdr_stereo_pcm_u8_dev(g_ctx, rf_decim, iq, npairs, 1, 2 * npairs, audio_up, audio_decim, audio_Fs, &taps,
+                                  &st, pcm, pcm_len),
+            "stereo_pcm_u8_dev");
+    check(sdr_copy_d2h_async(g_ctx, h_out[k], d_out[k], pcm_len * sizeof(int16_t)), "copy_d2h_async");
+  };
+  const char* nog = std::getenv("SDR_PROJECT_NO_GRAPH");
+  const bool use_graph = !(nog && std::atoi(nog) != 0);
+  sdr_graph* graph[2] = {nullptr, nullptr};
+
   auto flush = [&](unsigned b) {  // wait for block b and write its PCM (src/project.cpp:315)
     check(sdr_event_synchronize(g_ctx, done[b & 1]), "event_synchronize");
     std::fwrite(h_out[b & 1], sizeof(int16_t), pcm_len, stdout);
@@ -190,19 +214,16 @@ int main(int argc, char* argv[]) {
       std::cerr << "End of input stream reached" << std::endl;
       std::exit(1);  // as the reference (src/project.cpp:294-297)
     }
-    check(sdr_copy_h2d_async(g_ctx, d_in[k], h_in[k], block_size), "copy_h2d_async");
-    const uint8_t* iq = static_cast<const uint8_t*>(d_in[k]);
-    int16_t* pcm = static_cast<int16_t*>(d_out[k]);
-    if (mono)
-      check(sdr_mono_pcm_u8_dev(g_ctx, rf_decim, iq, npairs, 1, 2 * npairs, taps.h_rf, num_taps, st.state_i,
-                                st.state_q, st.ns_rf, st.prev_i, st.prev_q, st.delay_state, st.ns_delay, audio_up,
-                                audio_decim, taps.h_audio, audio_taps, st.state_audio, st.ns_audio, pcm, pcm_len),
-            "mono_pcm_u8_dev");
-    else
-      check(sdr_stereo_pcm_u8_dev(g_ctx, rf_decim, iq, npairs, 1, 2 * npairs, audio_up, audio_decim, audio_Fs, &taps,
-                                  &st, pcm, pcm_len),
-            "stereo_pcm_u8_dev");
-    check(sdr_copy_d2h_async(g_ctx, h_out[k], d_out[k], pcm_len * sizeof(int16_t)), "copy_d2h_async");
+    if (block_id == 0 || !use_graph) {
+      enqueue(k);  // the first block sizes the library's scratch (no allocation may happen inside a capture)
+    } else {
+      if (!graph[k]) {  // record slot k's sequence once, then replay it for every block in that slot
+        check(sdr_graph_begin(g_ctx), "graph_begin");
+        enqueue(k);
+        check(sdr_graph_end(g_ctx, &graph[k]), "graph_end");
+      }
+      check(sdr_graph_launch(g_ctx, graph[k]), "graph_launch");
+    }
     check(sdr_event_record(g_ctx, done[k]), "event_record");
     // block_id - 1's PCM goes out while the device runs block_id and the
     // next read waits on stdin

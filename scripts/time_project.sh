@@ -19,16 +19,20 @@ fs = {0: 2.4e6, 1: 1.44e6, 2: 2.4e6, 3: 1.92e6}[mode]
 fm_iq_u8(bb * nblk // 2, seed=5, fs=fs).tofile(path)
 PY
   for ch in mono stereo; do
-    for prog in oracle/_ref/project_ref 3dy4-real-time-software-defined-radio-_amd/sdr_project; do
-      name=$(basename $prog)
+    for v in ref graph direct; do
+      case $v in
+        ref) prog=oracle/_ref/project_ref; env=;;
+        graph) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_NO_GRAPH=0;;
+        direct) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_NO_GRAPH=1;;
+      esac
       t0=$(date +%s.%N)
-      timeout -k 10 300 $prog $mode $ch < "$OUT/in_$mode.u8" > "$OUT/out_${name}_${mode}_${ch}.s16" 2>/dev/null
+      env $env timeout -k 10 300 $prog $mode $ch < "$OUT/in_$mode.u8" > "$OUT/out_${v}_${mode}_${ch}.s16" 2>/dev/null
       rc=$?
       t1=$(date +%s.%N)
-      [ $rc -eq 1 ] || { echo "$name rc=$rc"; exit 1; }
-      echo "mode $mode $ch $name: $(python3 -c "print(f'{$t1-$t0:.3f}')") s for $NBLK blocks"
+      [ $rc -eq 1 ] || { echo "$v rc=$rc"; exit 1; }
+      echo "mode $mode $ch $v: $(python3 -c "print(f'{$t1-$t0:.3f}')") s for $NBLK blocks"
+      [ $v = ref ] || { cmp -s "$OUT/out_ref_${mode}_${ch}.s16" "$OUT/out_${v}_${mode}_${ch}.s16" && echo "  outputs identical" || { echo "  OUTPUTS DIFFER"; exit 1; }; }
     done
-    cmp -s "$OUT/out_project_ref_${mode}_${ch}.s16" "$OUT/out_sdr_project_${mode}_${ch}.s16" && echo "  outputs identical" || { echo "  OUTPUTS DIFFER"; exit 1; }
   done
 done
 rm -f "$OUT"/*.u8 "$OUT"/*.s16
