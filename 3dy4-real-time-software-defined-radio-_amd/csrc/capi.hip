@@ -543,8 +543,18 @@ int sdr_frontend_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
                       state_q, ns, prev_i, prev_q, demod, out_stride);
 }
 
+static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
+                        const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
+                        const float* lp_tables);
+
 int sdr_resample_f32_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                          const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
+  return resample_dev(c, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, nullptr);
+}
+
+static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
+                        const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
+                        const float* lp_tables) {
   int rc = enter(c);
   if (rc) return rc;
   if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
@@ -566,9 +576,65 @@ int sdr_resample_f32_dev(sdr_ctx* c, int up, int down, const float* x, long long
   float* hp = static_cast<float*>(scratch(c, kTmp, sdr::resample_scratch_floats(up, ntaps) * sizeof(float)));
   if (!hp) return fail(c, SDR_ENOMEM, "polyphase table");
   hipError_t e = sdr::launch_resample(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, hp,
-                                      c->cur);
+                                      c->cur, lp_tables);
   if (e != hipSuccess) return hip_fail(c, e, "resample launch");
   return SDR_OK;
+}
+
+struct sdr_resample_plan {
+  int up = 0, down = 0, ntaps = 0;
+  const float* h = nullptr;
+  float* tables = nullptr;  // resample_lp's tables, or nullptr when the shape takes another kernel
+};
+
+int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int ntaps, sdr_resample_plan** out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!out || !h) return fail(c, SDR_EINVAL, "null pointer");
+  *out = nullptr;
+  if (up < 1 || down < 1 || ntaps < 1) return fail(c, SDR_EINVAL, "up/down/ntaps must be >= 1");
+  auto* p = new sdr_resample_plan;
+  p->up = up;
+  p->down = down;
+  p->ntaps = ntaps;
+  p->h = h;
+  if (up > 1) {
+    const size_t bytes = sdr::resample_rs_scratch_floats(up, ntaps) * sizeof(float);
+    hipError_t e = hipMalloc(&p->tables, bytes);
+    if (e != hipSuccess) {
+      delete p;
+      return fail(c, SDR_ENOMEM, "resample plan tables");
+    }
+    if (!sdr::resample_lp_tables(up, down, h, ntaps, 0, p->tables, c->cur, &e)) {
+      (void)hipFree(p->tables);
+      p->tables = nullptr;  // another kernel: built per call as before
+    } else if (e != hipSuccess) {
+      (void)hipFree(p->tables);
+      delete p;
+      return hip_fail(c, e, "resample plan tables");
+    }
+  }
+  *out = p;
+  return SDR_OK;
+}
+
+int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (p) {
+    if (p->tables) {
+      (void)hipStreamSynchronize(c->cur);
+      (void)hipFree(p->tables);
+    }
+    delete p;
+  }
+  return SDR_OK;
+}
+
+int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const float* x, long long n, int nstreams,
+                              long long x_stride, float* state, int ns, float* y, long long y_stride) {
+  if (!p) return fail(c, SDR_EINVAL, "null plan");
+  return resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->tables);
 }
 
 int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,

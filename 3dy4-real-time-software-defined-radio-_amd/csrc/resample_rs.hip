@@ -587,9 +587,27 @@ size_t resample_rs_scratch_floats(int up, int ntaps) {
 
 // Returns false (nothing launched) when the shape is not one this kernel
 // covers; the caller then takes the phase-major kernel of resample.hip.
+bool resample_lp_tables(int up, int down, const float* h, int ntaps, int ns, float* tables, hipStream_t st,
+                        hipError_t* err) {
+  const int cmax = (ntaps + up - 1) / up;
+  if (up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
+  const int base0 = -(((cmax - 1) + 3) / 4 * 4);
+  const int qmax = (int)((long long)(up - 1) * down / up);
+  if (!(up <= kLpSlots && (long long)up * down < (1LL << 31) && qmax + 1 - base0 + 4 <= kLpBuf && ns <= kLpSlots))
+    return false;
+  const int S = kLpSlots / up;
+  const int U = (cmax + 6) / 4 * 4;
+  const long long tab = 4LL * up * U;
+  int* lanes = reinterpret_cast<int*>(tables + tab);
+  hipLaunchKernelGGL(build_lp_tables, dim3((unsigned)((tab + kLpSlots - 1) / kLpSlots + 1)), dim3(kLpSlots), 0, st, h,
+                     up, down, cmax, U, S, base0, tables, lanes);
+  *err = hipGetLastError();
+  return true;
+}
+
 bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
-                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done) {
+                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done, const float* lp_tables) {
   *state_done = false;
   const int cmax = (ntaps + up - 1) / up;
   if (up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
@@ -621,8 +639,10 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       b.x = x;
       b.n = n;
       b.x_stride = x_stride;
-      b.hs = scratch;
-      b.lanes = reinterpret_cast<const int*>(scratch + 4LL * up * ((cmax + 6) / 4 * 4));
+      // tables built once by a plan (resample_lp_tables), or here for this call
+      const float* tables = lp_tables ? lp_tables : scratch;
+      b.hs = tables;
+      b.lanes = reinterpret_cast<const int*>(tables + 4LL * up * ((cmax + 6) / 4 * 4));
       b.up = up;
       b.down = down;
       b.state = state;
@@ -638,9 +658,11 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       b.ablate = ablate;
       const int U = (cmax + 6) / 4 * 4;
       const long long tab = 4LL * up * U;
-      hipLaunchKernelGGL(build_lp_tables, dim3((unsigned)((tab + kLpSlots - 1) / kLpSlots + 1)), dim3(kLpSlots), 0, st,
-                         h, up, down, cmax, U, S, base0, scratch, const_cast<int*>(b.lanes));
-      if ((*err = hipGetLastError()) != hipSuccess) return true;
+      if (!lp_tables) {
+        hipLaunchKernelGGL(build_lp_tables, dim3((unsigned)((tab + kLpSlots - 1) / kLpSlots + 1)), dim3(kLpSlots), 0,
+                           st, h, up, down, cmax, U, S, base0, scratch, reinterpret_cast<int*>(scratch + tab));
+        if ((*err = hipGetLastError()) != hipSuccess) return true;
+      }
       const int grid = b.nitems < ncu ? b.nitems : ncu;
       if (cmax == 151) {
         if (K == 4)

@@ -73,9 +73,11 @@ hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, S
                       float* scratch_y0, float* scratch_y1, bool allow_fast);
 hipError_t launch_demod(const float* I, const float* Q, long long n, int nstreams, long long stride,
                         float* prev_i, float* prev_q, float* out, long long out_stride, hipStream_t st);
+// lp_tables: resample_lp's tables prebuilt by resample_lp_tables (a plan),
+// or nullptr to build them into scratch_taps for this call
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                           long long ny, float* scratch_taps, hipStream_t st);
+                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables = nullptr);
 hipError_t launch_delay(const float* in, long long n, int nstreams, long long in_stride, float* state, int ns,
                         float* out, long long out_stride, hipStream_t st);
 hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
@@ -133,6 +135,12 @@ size_t resample_scratch_floats(int up, int ntaps);
 size_t resample_rs_scratch_floats(int up, int ntaps);
 bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
-                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done);
+                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done,
+                        const float* lp_tables = nullptr);
+// Build resample_lp's tables (shifted tap rows + lane table, resample_rs_scratch_floats
+// floats) once for a plan; false (nothing launched) when the shape is not one
+// resample_lp covers.
+bool resample_lp_tables(int up, int down, const float* h, int ntaps, int ns, float* tables, hipStream_t st,
+                        hipError_t* err);
 
 }  // namespace sdr

@@ -86,6 +86,9 @@ _SIGS = {
     "sdr_frontend_f32_dev": [_vp, _i, _vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _ll],
     "sdr_frontend_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _ll],
     "sdr_resample_f32_dev": [_vp, _i, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_resample_plan_create": [_vp, _i, _i, _vp, _i, C.POINTER(_vp)],
+    "sdr_resample_plan_f32_dev": [_vp, _vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
+    "sdr_resample_plan_destroy": [_vp, _vp],
     "sdr_fir_block_f16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
     "sdr_f32_to_f16_dev": [_vp, _vp, _ll, _vp],
     "sdr_delay_f32_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
@@ -205,6 +208,22 @@ class Graph:
         if self._g:
             lib().sdr_graph_destroy(self._ctx._c, self._g)
             self._g = _vp()
+
+
+class ResamplePlan:
+    """sdr_resample_plan: resample_dev with the tap tables built once."""
+
+    def __init__(self, ctx: "Context", p):
+        self._ctx, self._p = ctx, p
+
+    def resample_dev(self, x, n, nstreams, x_stride, state, ns, y, y_stride):
+        self._ctx._check(lib().sdr_resample_plan_f32_dev(self._ctx._c, self._p, _ptr(x), n, nstreams, x_stride,
+                                                         _ptr(state), ns, _ptr(y), y_stride), "resample_plan_dev")
+
+    def close(self):
+        if self._p:
+            lib().sdr_resample_plan_destroy(self._ctx._c, self._p)
+            self._p = _vp()
 
 
 class Context:
@@ -356,6 +375,12 @@ class Context:
     def resample_dev(self, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
         self._check(lib().sdr_resample_f32_dev(self._c, up, down, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
                                                _ptr(state), ns, _ptr(y), y_stride), "resample_dev")
+
+    def resample_plan(self, up, down, h, ntaps) -> "ResamplePlan":
+        """sdr_resample_plan_create: the lane-phase kernel's tables built once from device taps h."""
+        p = _vp()
+        self._check(lib().sdr_resample_plan_create(self._c, up, down, _ptr(h), ntaps, C.byref(p)), "resample_plan")
+        return ResamplePlan(self, p)
 
     def fir_block_f16_dev(self, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride):
         """fp16-storage arm of blockConvolveFIR (tolerance, not bit-exact)."""

@@ -334,8 +334,12 @@ class Job:
             ny = sdrhip.resample_out_len(up, down, n)
             out = torch.empty(S * ny, dtype=torch.float32, device=dev)
             self.keep.append(out)
+            # a plan: the tap tables are built once (sdr_resample_plan_create), as a
+            # streaming receiver with fixed taps does; one launch per step
+            plan = ctx.resample_plan(up, down, d_h, T)
+            self.keep.append(plan)
             for I, _ in planar:
-                steps.append(lambda I=I: ctx.resample_dev(up, down, I, n, S, n, d_h, T, st0, ns, out, ny))
+                steps.append(lambda I=I: plan.resample_dev(I, n, S, n, st0, ns, out, ny))
             self.units = S * n  # input samples per step
             self.bytes_per_pair = 4.0 + 4.0 * up / down
             self.flops_per_unit = 2.0 * (T / up) * up / down
@@ -448,6 +452,9 @@ class Job:
             self.graph[0].close()
             self.graph = None
         self.torch.cuda.synchronize(self.dev)
+        for k in self.keep:
+            if hasattr(k, "close"):
+                k.close()
         self.ctx.close()
 
 

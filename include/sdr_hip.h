@@ -171,6 +171,22 @@ int sdr_resample_f32_dev(sdr_ctx *ctx, int up, int down, const float *x, long lo
                          long long x_stride, const float *h, int ntaps, float *state, int ns, float *y,
                          long long y_stride);
 
+/* A resampler plan: the lane-phase kernel's tap tables (each phase's taps,
+ * pre-shifted per window alignment, and the bank-aware lane table) built
+ * ONCE from the device taps h, instead of by a small launch in every
+ * sdr_resample_f32_dev call.  A streaming caller's taps do not change
+ * (src/project.cpp:262-266 designs them once), so the per-block call is a
+ * single launch.  h is read at creation by that kernel and at each call by
+ * the fallback kernels (other shapes): it must not change while the plan
+ * lives.  Same outputs, state and preconditions as sdr_resample_f32_dev. */
+typedef struct sdr_resample_plan sdr_resample_plan;
+int sdr_resample_plan_create(sdr_ctx *ctx, int up, int down, const float *h, int ntaps,
+                             sdr_resample_plan **plan);
+int sdr_resample_plan_f32_dev(sdr_ctx *ctx, const sdr_resample_plan *plan, const float *x, long long n,
+                              int nstreams, long long x_stride, float *state, int ns, float *y,
+                              long long y_stride);
+int sdr_resample_plan_destroy(sdr_ctx *ctx, sdr_resample_plan *plan);
+
 /* BASELINE config 5's fp16 arm of blockConvolveFIR (src/filter.cpp:66-83):
  * x and state are fp16 (IEEE binary16, [nstreams][x_stride] / [nstreams][ns]),
  * taps fp32 (rounded to fp16 inside), y fp32.  fp32 accumulation of fp16

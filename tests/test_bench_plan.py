@@ -95,3 +95,67 @@ def test_thread_driver_collects_every_device(monkeypatch):
     assert out["n_gpus"] == 4 and out["config"]["devices_opened"] == 4
     assert out["ms_per_step"] == pytest.approx(0.4)  # the slowest device: 4 ms / 10 steps
     assert len(out["per_gpu"]["value"]) == 4
+
+
+def _rank_main(rank, world, port, q):
+    """One torch.distributed.run rank of bench.main() with a fake device runner."""
+    import importlib.util
+    import io
+    import json
+    import os
+    import sys
+
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+
+    def fake_run_device(cfg, device, seed, args, barrier=None, side=True):
+        assert device == rank and not side
+        barrier()  # the gloo barrier the real timed region uses
+        job = {"units": 1000, "bytes_per_pair": 8.4, "flops_per_unit": 41.4, "metric": "m", "bound": "hbm",
+               "kind": "frontend_f32", "tolerance": None}
+        return {"device": device, "ms": 2.0 + rank, "wall": 0.01, "job": job}
+
+    b.run_device = fake_run_device
+    import torch
+
+    torch.cuda.device_count = lambda: world
+    out = io.StringIO()
+    sys.stdout = out
+    try:
+        b.main(["--gpus", str(world), "--steps", "10", "--no-cpu-baseline"])
+    finally:
+        sys.stdout = sys.__stdout__
+    text = out.getvalue().strip()
+    q.put((rank, json.loads(text) if text else None))
+
+
+def test_torchrun_ranks_use_gloo_and_max_time():
+    """The torch.distributed.run path: each rank one device, the barrier and
+    the max-over-ranks over a CPU gloo group (no device collective); rank 0
+    alone prints, with the slowest rank's time."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[1] is None  # only rank 0 prints
+    line = got[0]
+    assert line["n_gpus"] == 2 and line["config"]["devices_opened"] == 2
+    assert line["ms_per_step"] == pytest.approx(0.3)  # max(2, 3) ms / 10 steps
+    assert line["per_gpu"]["ms_per_step"] == [pytest.approx(0.2), pytest.approx(0.3)]
+    assert "gloo" in line["config"]["parallelism"]

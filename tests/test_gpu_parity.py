@@ -482,3 +482,34 @@ def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix, n):
             want = oracle.pointwise_mul(nco, mb[s]) if mix else nco
             assert_bits(got[s], want, f"stream {s} block {b}")
             assert_bits(dev_st[s], ost[s], f"pll state stream {s} block {b}")
+
+
+@pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
+                                             (147, 1280, 101, 100, 12800), (3, 5, 101, 100, 5000)])
+def test_resample_plan_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, n):
+    """sdr_resample_plan_*: the lane-phase tables built once at plan creation,
+    then three consecutive blocks through the plan -- outputs and carried
+    state bitwise against the oracle.  (3, 5) is a shape the lane-phase
+    kernel does not take: the plan falls back to the per-call path."""
+    sdrhip = built_lib
+    nstreams = 3
+    rng = np.random.default_rng(up + down + cnt)
+    h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
+    ny = sdrhip.resample_out_len(up, down, n)
+    states = [rng.standard_normal(ns).astype(np.float32) for _ in range(nstreams)]
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_st = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.stack(states))
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * ny * 4)
+    plan = gpu_ctx.resample_plan(up, down, d_h, len(h))
+    try:
+        for blk in range(3):
+            x = rng.standard_normal((nstreams, n)).astype(np.float32)
+            d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+            plan.resample_dev(d_x, n, nstreams, n, d_st, ns, d_y, ny)
+            gpu_ctx.synchronize()
+            got = d_y.download().reshape(nstreams, ny)
+            for s in range(nstreams):
+                assert_bits(got[s], oracle.resample(up, down, x[s], h, states[s]), f"stream {s} block {blk}")
+            assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
+    finally:
+        plan.close()
