@@ -789,11 +789,21 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
   if ((rc = sdr_frontend_u8_dev(c, D, iq, npairs, nstreams, iq_stride, taps->h_rf, taps->rf_taps, st->state_i,
                                 st->state_q, st->ns_rf, st->prev_i, st->prev_q, demod, dstride)))
     return rc;
-  SDR_HIP(c, hipEventRecord(c->fork, c->cur));
-  SDR_HIP(c, hipStreamWaitEvent(c->side, c->fork, 0));
+  // Fork only while the recurrence (one lane per stream, 64 streams per
+  // wave) leaves most of the chip idle: at 1,024 streams (16 waves) the side
+  // branch runs in the gaps (stereo0 -1.6 %), at 16,384 (256 waves, one per
+  // CU) it competes with the latency-bound recurrence for the CUs and slows
+  // it (stereo0w +14 %, same box).  SDR_STEREO_FORK=0/1 forces either way.
+  static const int fork_env = sdr::env_int("SDR_STEREO_FORK", -1);
+  const long long pll_waves = (nstreams + 63) / 64;
+  const bool fork = fork_env >= 0 ? fork_env != 0 : 4 * pll_waves <= sdr::device_cu_count();
+  if (fork) {
+    SDR_HIP(c, hipEventRecord(c->fork, c->cur));
+    SDR_HIP(c, hipStreamWaitEvent(c->side, c->fork, 0));
+  }
   {
     hipStream_t main = c->cur;
-    c->cur = c->side;
+    if (fork) c->cur = c->side;
     // :114-116: mono = resample(delay(demod)); :121: stereo band-pass
     rc = sdr_delay_f32_dev(c, demod, nd, nstreams, dstride, st->delay_state, st->ns_delay, delayed, dstride);
     if (!rc)
@@ -802,7 +812,7 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
     if (!rc)
       rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_stereo, taps->bpf_taps, st->stereo_state,
                                  st->ns_bpf, sband, dstride);
-    hipError_t e = rc ? hipSuccess : hipEventRecord(c->join, c->side);
+    hipError_t e = (rc || !fork) ? hipSuccess : hipEventRecord(c->join, c->side);
     c->cur = main;
     if (rc) return rc;
     if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
@@ -816,7 +826,7 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
                                             args, pstride, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "pll launch");
   // join: the NCO mixed with the stereo band (pointwiseMultiply x2, :127)
-  SDR_HIP(c, hipStreamWaitEvent(c->cur, c->join, 0));
+  if (fork) SDR_HIP(c, hipStreamWaitEvent(c->cur, c->join, 0));
   e = sdr::launch_nco(args, pstride, nd, nstreams, 2.0f, 0.0f, sband, dstride, mixed, dstride, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "nco launch");
   // :129: the stereo channel through the same audio resampler, its own state

@@ -10,8 +10,8 @@
 //   cpu_bench frontend <block_pairs> <seconds> <threads>
 //       the mode-0 front end (src/project.cpp:86-90: FIR+dec10 on I and Q,
 //       then fmDemodArctan) on independent synthetic streams, one stream per
-//       std::thread, one per core of the CPU share (<threads> = 0), each pinned to
-//       its own core of the affinity set.
+//       std::thread, one per core of the CPU share (<threads> = 0), pinned one per
+//       core when the whole affinity set is the share.
 //       Prints {"pairs":..., "seconds":..., "threads":...}.
 //   cpu_bench program <project_binary> <blocks> <procs>
 //       BASELINE config 1: `<project_binary> 0 mono` (the reference program,
@@ -184,10 +184,15 @@ int run_frontend(long n, double seconds, int threads) {
   std::vector<std::thread> pool;
   for (int t = 0; t < threads; ++t) {
     pool.emplace_back([&, t] {
-      cpu_set_t one;
-      CPU_ZERO(&one);
-      CPU_SET(cpus[t % cpus.size()], &one);
-      pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+      // pin one thread per core only when the whole affinity set is ours; on
+      // a quota-limited share (a GPU box grants 16 of 256) the first cores of
+      // the set are not ours alone, and the scheduler places the threads
+      if (share.cores == (int)share.affinity && threads <= (int)cpus.size()) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpus[t % cpus.size()], &one);
+        pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+      }
       void* f = ref_front_new(h.data(), 101, 100);
       std::vector<float> demod(n / 10);
       ready.fetch_add(1);
