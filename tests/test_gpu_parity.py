@@ -152,8 +152,9 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
 RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
                   (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                   (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
-# resample_lp (default), then resample_rs, then the phase-major resample_pp
-RESAMPLE_KERNELS = {"lp": {}, "rs": {"SDR_RESAMPLE_LP": "0"},
+# resample_lp (default), the opt-in resample_sw, then resample_rs, the phase-major resample_pp
+RESAMPLE_KERNELS = {"lp": {}, "sw": {"SDR_RESAMPLE_SW": "1"},
+                    "rs": {"SDR_RESAMPLE_LP": "0"},
                     "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
 
 
@@ -188,6 +189,37 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
         for s in range(nstreams):
             assert_bits(got[s], oracle.resample(up, down, x[s], h, states[s]), f"stream {s} block {blk}")
         assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
+
+
+@pytest.mark.parametrize("up,down,cnt,nstreams,n", [(147, 800, 151, 130, 8000), (147, 800, 101, 64, 4000),
+                                                     (441, 3200, 101, 70, 6400), (147, 1280, 101, 3, 25600)])
+def test_resample_sw_lane_groups(gpu_ctx, oracle, built_lib, monkeypatch, up, down, cnt, nstreams, n):
+    """resample_sw with one lane per stream (>= 64 streams: several lane
+    groups, a partial last group) and with streams split into column runs;
+    three consecutive blocks, state carried; checked stream by stream
+    against the oracle (a random sample of streams when there are many)."""
+    monkeypatch.setenv("SDR_RESAMPLE_SW", "1")
+    sdrhip = built_lib
+    rng = np.random.default_rng(up + down + nstreams)
+    h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
+    ns = cnt - 1
+    ny = sdrhip.resample_out_len(up, down, n)
+    states = rng.standard_normal((nstreams, ns)).astype(np.float32)
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_st = sdrhip.DeviceArray.from_numpy(gpu_ctx, states)
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * ny * 4)
+    check = sorted(set([0, nstreams - 1] + list(rng.choice(nstreams, size=min(nstreams, 12), replace=False))))
+    for blk in range(3):
+        x = rng.standard_normal((nstreams, n)).astype(np.float32)
+        d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+        gpu_ctx.resample_dev(up, down, d_x, n, nstreams, n, d_h, len(h), d_st, ns, d_y, ny)
+        gpu_ctx.synchronize()
+        got = d_y.download().reshape(nstreams, ny)
+        for s in check:
+            ref_state = states[s].copy()
+            assert_bits(got[s], oracle.resample(up, down, x[s], h, ref_state), f"stream {s} block {blk}")
+        states = np.ascontiguousarray(x[:, n - ns:])
+        assert_bits(d_st.download().reshape(nstreams, ns), states, f"state block {blk}")
 
 
 @pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000)])

@@ -77,6 +77,14 @@ __global__ __launch_bounds__(256) void valu(float* out, int iters, float s) {
 #define A(V) { float t; asm volatile("v_mul_f32 %1, %2, %3\n\tv_add_f32 %0, %1, %0" : "+v"(V.x), "=&v"(t) : "s"(s), "v"(V.y)); }
       REP8(A(a0) A(a1) A(a2) A(a3) A(a4) A(a5) A(a6) A(a7))
 #undef A
+    } else if constexpr (OP == 15) {  // v_mul_f32_dpp row_newbcast (tap broadcast from a 16-lane row)
+#define A(V) asm volatile("v_mul_f32_dpp %0, %2, %0 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\tv_mul_f32_dpp %1, %2, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(V.x), "+v"(V.y) : "v"(c.y));
+      REP8(A(a0) A(a1) A(a2) A(a3) A(a4) A(a5) A(a6) A(a7))
+#undef A
+    } else if constexpr (OP == 16) {  // dpp mul + add, the add's chain dependent on the mul (resample_sw's MAC)
+#define A(V) { float t; asm volatile("v_mul_f32_dpp %1, %2, %3 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\tv_add_f32 %0, %1, %0" : "+v"(V.x), "=&v"(t) : "v"(c.y), "v"(V.y)); }
+      REP8(A(a0) A(a1) A(a2) A(a3) A(a4) A(a5) A(a6) A(a7))
+#undef A
     }
   }
   const f2 t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
@@ -97,9 +105,9 @@ int main() {
   const char* names[] = {"v_add_f32", "v_mul_f32 (s)", "v_fma_f32", "v_pk_add_f32", "v_pk_mul_f32 (s bcast)",
                          "v_pk_fma_f32", "pk_mul+pk_add", "mul+add",
                          "v_fma_f32 vvv", "v_mul_f32 vv", "v_fmac_f32 vv", "v_fmac_f32 sv", "v_add_f32 sv",
-                         "mul vv + add", "mul(s)+add (dep)"};
+                         "mul vv + add", "mul(s)+add (dep)", "v_mul_f32_dpp bcast", "mul_dpp+add (dep)"};
   const int iters = 2000;
-  for (int op = 0; op < 15; ++op) {
+  for (int op = 0; op < 17; ++op) {
     for (int w : {1, 2, 3, 4, 8}) {  // waves per SIMD (256-thread WGs = 1 wave per SIMD each)
       const int grid = ncu * w;
       auto launch = [&] {
@@ -119,6 +127,8 @@ int main() {
           case 12: hipLaunchKernelGGL(valu<12>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
           case 13: hipLaunchKernelGGL(valu<13>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
           case 14: hipLaunchKernelGGL(valu<14>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
+          case 15: hipLaunchKernelGGL(valu<15>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
+          case 16: hipLaunchKernelGGL(valu<16>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
         }
       };
       launch();
