@@ -545,16 +545,16 @@ int sdr_frontend_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
 
 static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                        const float* lp_tables, const float* sw_tables);
+                        const float* lp_tables);
 
 int sdr_resample_f32_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                          const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
-  return resample_dev(c, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, nullptr, nullptr);
+  return resample_dev(c, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, nullptr);
 }
 
 static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                        const float* lp_tables, const float* sw_tables) {
+                        const float* lp_tables) {
   int rc = enter(c);
   if (rc) return rc;
   if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
@@ -576,7 +576,7 @@ static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long 
   float* hp = static_cast<float*>(scratch(c, kTmp, sdr::resample_scratch_floats(up, ntaps) * sizeof(float)));
   if (!hp) return fail(c, SDR_ENOMEM, "polyphase table");
   hipError_t e = sdr::launch_resample(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, hp,
-                                      c->cur, lp_tables, sw_tables);
+                                      c->cur, lp_tables);
   if (e != hipSuccess) return hip_fail(c, e, "resample launch");
   return SDR_OK;
 }
@@ -584,11 +584,8 @@ static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long 
 struct sdr_resample_plan {
   int up = 0, down = 0, ntaps = 0;
   const float* h = nullptr;
-  float* tables = nullptr;     // resample_lp's tables, or nullptr when the shape takes another kernel
-  float* sw_tables = nullptr;  // resample_sw's padded tap table, or nullptr
+  float* tables = nullptr;  // resample_lp's tables, or nullptr when the shape takes another kernel
 };
-
-int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p);
 
 int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int ntaps, sdr_resample_plan** out) {
   int rc = enter(c);
@@ -602,32 +599,18 @@ int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int n
   p->ntaps = ntaps;
   p->h = h;
   if (up > 1) {
-    // resample_sw's table (the default kernel) and resample_lp's (taken when a
-    // call's buffers do not suit resample_sw), each built once here
-    if (sdr::sw_shape_ok(up, down, ntaps)) {
-      hipError_t e = hipMalloc(&p->sw_tables, sdr::sw_table_floats(up, ntaps) * sizeof(float));
-      if (e != hipSuccess) {
-        delete p;
-        return fail(c, SDR_ENOMEM, "resample plan tables");
-      }
-      if ((e = sdr::build_sw_table(up, down, h, ntaps, p->sw_tables, c->cur)) != hipSuccess) {
-        (void)hipFree(p->sw_tables);
-        delete p;
-        return hip_fail(c, e, "resample plan tables");
-      }
-    }
     const size_t bytes = sdr::resample_rs_scratch_floats(up, ntaps) * sizeof(float);
     hipError_t e = hipMalloc(&p->tables, bytes);
     if (e != hipSuccess) {
-      p->tables = nullptr;
-      sdr_resample_plan_destroy(c, p);
+      delete p;
       return fail(c, SDR_ENOMEM, "resample plan tables");
     }
     if (!sdr::resample_lp_tables(up, down, h, ntaps, 0, p->tables, c->cur, &e)) {
       (void)hipFree(p->tables);
       p->tables = nullptr;  // another kernel: built per call as before
     } else if (e != hipSuccess) {
-      sdr_resample_plan_destroy(c, p);
+      (void)hipFree(p->tables);
+      delete p;
       return hip_fail(c, e, "resample plan tables");
     }
   }
@@ -639,9 +622,10 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
   int rc = enter(c);
   if (rc) return rc;
   if (p) {
-    if (p->tables || p->sw_tables) (void)hipStreamSynchronize(c->cur);
-    if (p->tables) (void)hipFree(p->tables);
-    if (p->sw_tables) (void)hipFree(p->sw_tables);
+    if (p->tables) {
+      (void)hipStreamSynchronize(c->cur);
+      (void)hipFree(p->tables);
+    }
     delete p;
   }
   return SDR_OK;
@@ -650,8 +634,7 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
 int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const float* x, long long n, int nstreams,
                               long long x_stride, float* state, int ns, float* y, long long y_stride) {
   if (!p) return fail(c, SDR_EINVAL, "null plan");
-  return resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->tables,
-                      p->sw_tables);
+  return resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->tables);
 }
 
 int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,

@@ -325,21 +325,18 @@ size_t resample_scratch_floats(int up, int ntaps) {
   const int cmax = (ntaps + up - 1) / up;
   const size_t pp = (size_t)up * (size_t)((cmax + 3) / 4 * 4);
   const size_t rs = resample_rs_scratch_floats(up, ntaps);
-  const size_t sw = sw_table_floats(up, ntaps);
-  const size_t m = pp > rs ? pp : rs;
-  return m > sw ? m : sw;
+  return pp > rs ? pp : rs;
 }
 
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables,
-                           const float* sw_tables) {
+                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables) {
   {
     // resample_rs.hip's kernels first (lane-phase, then sliding-window), for the shapes they cover
     hipError_t e = hipSuccess;
     bool state_done = false;
     if (launch_resample_rs(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, scratch_taps,
-                           st, &e, &state_done, lp_tables, sw_tables)) {
+                           st, &e, &state_done, lp_tables)) {
       if (e != hipSuccess || ns <= 0 || state_done) return e;
       hipLaunchKernelGGL(resample_commit, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st, x, n,
                          x_stride, state, ns);

@@ -607,24 +607,10 @@ bool resample_lp_tables(int up, int down, const float* h, int ntaps, int ns, flo
 
 bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
-                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done, const float* lp_tables,
-                        const float* sw_tables) {
+                        float* scratch, hipStream_t st, hipError_t* err, bool* state_done, const float* lp_tables) {
   *state_done = false;
   const int cmax = (ntaps + up - 1) / up;
   if (up < 2 || ntaps != cmax * up || (cmax != 151 && cmax != 101) || down % 4 != 0) return false;
-  // resample_sw (resample_sw.hip) first: its tap table from the plan, or
-  // built here for this call
-  if (sw_covers(up, down, ntaps, x, nstreams, x_stride)) {
-    const float* tab = sw_tables;
-    if (!tab) {
-      if ((*err = build_sw_table(up, down, h, ntaps, scratch, st)) != hipSuccess) return true;
-      tab = scratch;
-    }
-    if (launch_resample_sw(up, down, x, n, nstreams, x_stride, ntaps, tab, state, ns, y, y_stride, ny, st, err)) {
-      *state_done = true;  // resample_sw commits the state itself
-      return true;
-    }
-  }
   // 16-B chunks straight from the rows
   if ((reinterpret_cast<uintptr_t>(x) & 15) || (nstreams > 1 && x_stride % 4)) return false;
   // resample_lp: the staging buffer must hold at least one column's span

@@ -77,8 +77,7 @@ hipError_t launch_demod(const float* I, const float* Q, long long n, int nstream
 // or nullptr to build them into scratch_taps for this call
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables = nullptr,
-                           const float* sw_tables = nullptr);
+                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables = nullptr);
 hipError_t launch_delay(const float* in, long long n, int nstreams, long long in_stride, float* state, int ns,
                         float* out, long long out_stride, hipStream_t st);
 hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
@@ -137,18 +136,7 @@ size_t resample_rs_scratch_floats(int up, int ntaps);
 bool launch_resample_rs(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
                         float* scratch, hipStream_t st, hipError_t* err, bool* state_done,
-                        const float* lp_tables = nullptr, const float* sw_tables = nullptr);
-// Sliding-window resampler, lane = stream segment (resample_sw.hip): whether
-// it covers the shape, and the launch over prebuilt shifted rows hs[4][L][U]
-// (false = not launched).  It commits the new state itself.
-bool sw_shape_ok(int up, int down, int ntaps);
-bool sw_covers(int up, int down, int ntaps, const float* x, int nstreams, long long x_stride);
-// its padded tap table (sw_table_floats floats), built once by a plan or per call
-size_t sw_table_floats(int up, int ntaps);
-hipError_t build_sw_table(int up, int down, const float* h, int ntaps, float* table, hipStream_t st);
-bool launch_resample_sw(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
-                        int ntaps, const float* table, float* state, int ns, float* y, long long y_stride,
-                        long long ny, hipStream_t st, hipError_t* err);
+                        const float* lp_tables = nullptr);
 // Build resample_lp's tables (shifted tap rows + lane table, resample_rs_scratch_floats
 // floats) once for a plan; false (nothing launched) when the shape is not one
 // resample_lp covers.

@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider -rf --timeout 120 \
   --timeout-method thread -k "${TESTK:-resample}" > "$OUT/pytest.log" 2>&1
 rc=$?; tail -15 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
-for kv in "lp:" "sw:SDR_RESAMPLE_SW=1"; do
+for kv in "lp:" "rs:SDR_RESAMPLE_LP=0"; do
   name=${kv%%:*}; env=${kv#*:}
   env $env timeout -k 10 300 python bench.py --config cfg3 --steps 100 --warmup 3 --no-cpu-baseline \
     > "$OUT/bench_cfg3_$name.json" 2>> "$OUT/bench.err"

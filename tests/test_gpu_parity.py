@@ -152,9 +152,8 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
 RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
                   (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                   (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
-# resample_lp (default), the opt-in resample_sw, then resample_rs, the phase-major resample_pp
-RESAMPLE_KERNELS = {"lp": {}, "sw": {"SDR_RESAMPLE_SW": "1"},
-                    "rs": {"SDR_RESAMPLE_LP": "0"},
+# resample_lp (default), then resample_rs, then the phase-major resample_pp
+RESAMPLE_KERNELS = {"lp": {}, "rs": {"SDR_RESAMPLE_LP": "0"},
                     "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
 
 
@@ -193,12 +192,12 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
 
 @pytest.mark.parametrize("up,down,cnt,nstreams,n", [(147, 800, 151, 130, 8000), (147, 800, 101, 64, 4000),
                                                      (441, 3200, 101, 70, 6400), (147, 1280, 101, 3, 25600)])
-def test_resample_sw_lane_groups(gpu_ctx, oracle, built_lib, monkeypatch, up, down, cnt, nstreams, n):
-    """resample_sw with one lane per stream (>= 64 streams: several lane
-    groups, a partial last group) and with streams split into column runs;
-    three consecutive blocks, state carried; checked stream by stream
-    against the oracle (a random sample of streams when there are many)."""
-    monkeypatch.setenv("SDR_RESAMPLE_SW", "1")
+def test_resample_many_streams(gpu_ctx, oracle, built_lib, up, down, cnt, nstreams, n):
+    """The default resampler over many streams per launch (64-130: several
+    workgroups' item ranges, items starting inside the carried state, a
+    ragged last batch) and over few long streams; three consecutive blocks,
+    state carried; checked stream by stream against the oracle (a random
+    sample of streams when there are many)."""
     sdrhip = built_lib
     rng = np.random.default_rng(up + down + nstreams)
     h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
