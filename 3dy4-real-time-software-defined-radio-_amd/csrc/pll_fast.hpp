@@ -1,0 +1,186 @@
+// pll_fast.hpp -- short-chain atan2 / sincos for the fmPLL recurrence, with a
+// certificate that the float the reference stores is the one computed.
+//
+// The reference evaluates errorD = atan2(errorQ, errorI) and
+// feedbackI/Q = cos/sin(trigArg) in double on float arguments and rounds each
+// result to float (src/filter.cpp:199, :216-217).  Only those floats feed the
+// recurrence, so any double approximation d of the exact value f gives the
+// same float as long as no float rounding boundary (a midpoint between two
+// adjacent floats) lies between d and f, nor between f and the library's
+// double result.  These routines keep the library's algorithms (OCML's
+// atan2/sincos polynomial coefficients) with fewer instructions and shorter
+// dependency chains -- one wave per SIMD issues every instruction of the
+// recurrence on its own, so the count is what the time is:
+//   - atan2: v/u by one reciprocal and a second-order correction instead of
+//     the IEEE division sequence; a degree-15 polynomial in t^2 (error
+//     < 2^-46.8) by Estrin's scheme (depth 5) instead of OCML's degree 19 by
+//     Horner's (depth 20);
+//   - sincos: a three-term FMA Cody-Waite reduction of the fp32 argument
+//     (exact first step) instead of the double-double reduction; the sine and
+//     cosine kernels by Estrin's scheme; quadrant signs applied to the floats.
+// Each double result is within ~2^-46.5 (relative) of the exact value: the
+// atan polynomial's fit error plus a few ulps of rounding (tests/pll_cert.cpp).
+//
+// Certificate.  mid_score() measures a result's distance to the nearest float
+// midpoint; the caller keeps the running unsigned minimum over a chunk, which
+// is certified while it stays >= kCertified, i.e. every result lies more than
+// 4,095 double ulps (~2^-40 relative) from a midpoint -- so it, the exact
+// value and the library's result (within ~2^-46.5 and 1-2 ulps of the exact
+// value) round to one float.  The remaining cases are guarded by chunk_ok on the
+// state before and after each chunk (finite and in range, so |trigArg| <
+// 2^26, trigArg != -0, the feedback floats are 0 or >= 2^-60, and errorD is
+// never subnormal; a NaN from x = y = 0 or a non-finite input reaches
+// phaseEst and fails the closing check).  Within those guards a certified
+// step's floats are the reference's; an uncertified chunk is re-run with the
+// library routines.  DESIGN.md section 4.7 has the argument.
+//
+// Host/device: SDR_HD is __host__ __device__ under hipcc; the CPU test of the
+// certificate (tests/pll_cert.cpp) defines it empty.  Ops supplies fma(a, b, c)
+// and rcp(u) (relative error <= 2^-20): the kernel's are a VOP3 v_fma_f64
+// (one instruction; the compiler's VOP2 fmac form costs a v_mov_b64 per
+// polynomial pair) and v_rcp_f64; the CPU test's are std fma and a
+// deliberately coarse reciprocal.
+#pragma once
+
+#ifndef SDR_HD
+#define SDR_HD __host__ __device__
+#endif
+
+namespace sdr {
+namespace pllfast {
+// atan(t) = t + t*z*P(z), z = t^2, t in [0, 1], P of degree 15: a weighted
+// least-squares fit (scripts/fit_atan.py) with relative error < 2^-46.8 on
+// [0, 1] -- 4 terms fewer than OCML's degree 19 (< 2^-54), well inside the
+// certificate's 2^-40 margin.  Coefficients c0..c15.
+constexpr double kAtanC[16] = {
+    -0x1.5555555548634p-2, 0x1.9999998dcb71cp-3, -0x1.2492473aa1d47p-3, 0x1.c71c204d48085p-4,
+    -0x1.7459013f32a55p-4, 0x1.3af102625a079p-4, -0x1.1042b16ee39eep-4, 0x1.dae1c88757e5cp-5,
+    -0x1.9852ad76ae65cp-5, 0x1.4cd7d6822d40bp-5, -0x1.e72bb0e3e1c37p-6, 0x1.2c694cfa120d0p-6,
+    -0x1.231ab51098098p-7, 0x1.97372e16c0db6p-9, -0x1.68e74a9b5111ap-11, 0x1.2ddb1bd53fd3fp-14};
+// OCML's (fdlibm's) sine / cosine kernels on [-pi/4, pi/4]
+constexpr double kS1 = -0x1.5555555555555p-3, kS2 = 0x1.1111111110bb3p-7, kS3 = -0x1.a01a019e83e5cp-13,
+                 kS4 = 0x1.71de3796cde01p-19, kS5 = -0x1.ae600b42fdfa7p-26, kS6 = 0x1.5e0b2f9a43bb8p-33;
+constexpr double kC1 = 0x1.5555555555555p-5, kC2 = -0x1.6c16c16c16967p-10, kC3 = 0x1.a01a019f4ec90p-16,
+                 kC4 = -0x1.27e4fa17f65f6p-22, kC5 = 0x1.1eeb69037ab78p-29, kC6 = -0x1.907db46cc5e42p-37;
+// pi/2 = P1 + P2 (+ -1.5e-33); 2/pi; pi.  A third Cody-Waite term is not
+// needed: over every float in [pi/4, 2^26) the reduced argument is at least
+// 2^-27.83 (exhaustive search, at x = 0x1.f9cbe2p+7), so |kd| * 1.5e-33 <=
+// 2^-84 changes none of them (scripts/min_reduced_arg.c).
+constexpr double kP1 = 0x1.921fb54442d18p+0, kP2 = 0x1.1a62633145c07p-54;
+constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
+constexpr double kPi = 0x1.921fb54442d18p+1;
+
+// mid_score(d) = ((lo29 - (2^28 - 4096)) mod 2^29) << 3 for the 29 mantissa
+// bits double -> float drops: < kCertified <=> lo29 within [-4096, 4096) of
+// the midpoint 2^28.  One shift-add per result.
+constexpr unsigned kCertified = 8192u << 3;
+constexpr unsigned kMidBias = 0x80008000u;  // -((2^28 - 4096) << 3) mod 2^32
+
+SDR_HD inline unsigned lo_bits(double d) { return (unsigned)__builtin_bit_cast(unsigned long long, d); }
+SDR_HD inline unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
+SDR_HD inline unsigned mid_score(double d) { return (lo_bits(d) << 3) + kMidBias; }
+
+// Chunk guard: the state at a chunk's start keeps every step of the next 8
+// inside the certified domain (|Kp|, |Ki| <= 1 is the caller's launch-time
+// condition).  Written with & so it is straight-line code.
+SDR_HD inline bool chunk_ok(float fbI, float fbQ, float integrator, float phaseEst, float trigOffset) {
+  const float aI = __builtin_fabsf(fbI), aQ = __builtin_fabsf(fbQ);
+  return (int)(trigOffset >= 0.0f) & (int)(trigOffset < 0x1p24f) & (int)(__builtin_fabsf(phaseEst) < 0x1p24f) &
+         (int)(__builtin_fabsf(integrator) < 0x1p20f) & (int)(aI <= 1.0f) & (int)(aQ <= 1.0f) &
+         ((int)(aI >= 0x1p-60f) | (int)(fbI == 0.0f)) & ((int)(aQ >= 0x1p-60f) | (int)(fbQ == 0.0f));
+}
+
+// A float that is NaN, Inf or subnormal.  In chunk_ok's domain errorD is
+// never subnormal (|errorQ / errorI| >= 2^-83 unless errorQ = 0, then the
+// result is exact) and x = y = 0 or a non-finite input gives NaN, which
+// reaches phaseEst and fails the chunk's closing chunk_ok; the CPU test
+// checks these claims with this predicate.
+SDR_HD inline bool float_special(float f) {
+  const unsigned e = __builtin_bit_cast(unsigned, f) >> 23 & 0xffu;
+  return (e == 0xffu) | ((e == 0u) & (__builtin_bit_cast(unsigned, f) << 1 != 0u));
+}
+
+// (float)atan2(y, x) for fp32 y, x: OCML's algorithm with fewer double
+// operations; folds the double result's midpoint distance into score.  A
+// double op is what the recurrence pays for (a single wave issues each one
+// on its own), so the float parts stay float: |x|, |y|, their max / min and
+// the quadrant tests are exact in fp32.
+template <class Ops>
+SDR_HD inline double atan2_abs(float y, float x, unsigned& score);
+template <class Ops>
+SDR_HD inline float atan2_fast(float y, float x, unsigned& score) {
+  return __builtin_copysignf((float)atan2_abs<Ops>(y, x, score), y);
+}
+// |atan2(y, x)| in double (the CPU test reads it to bound the error)
+template <class Ops>
+SDR_HD inline double atan2_abs(float y, float x, unsigned& score) {
+  const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+  const double u = (double)__builtin_fmaxf(ax, ay), v = (double)__builtin_fminf(ax, ay);
+  // v / u: r0 = (1 - e) / u exactly with |e| <= 2^-24.37 (v_rcp_f64, measured),
+  // so t = q0 (1 + e) = v/u (1 - e^2): relative error <= 2^-48.7 + 2 ulp
+  const double r0 = Ops::rcp(u);
+  const double q0 = v * r0;
+  const double e = Ops::fma(-u, r0, 1.0);
+  const double t = Ops::fma(q0, e, q0);
+  // P(z): the pairs c_2i + c_2i+1 z, then Horner in z^2
+  const double z = t * t;
+  const double z2 = z * z;
+  double p[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p[i] = Ops::fma(kAtanC[2 * i + 1], z, kAtanC[2 * i]);
+  double P = p[7];
+#pragma unroll
+  for (int i = 6; i >= 0; --i) P = Ops::fma(P, z2, p[i]);
+  // OCML's fixups (|y| > |x|: pi/2 - a; x negative (sign bit): pi - that) on
+  // a = t + t z P, folded into C + s (t + t z P) with s = +-1:
+  //   (swap, neg) = (0,0): 0 + a, (1,0): pi/2 - a, (0,1): pi - a, (1,1): pi/2 + a
+  const bool swap = ay > ax, neg = __builtin_signbit(x);
+  const double C = swap ? kP1 : (neg ? kPi : 0.0);
+  const unsigned long long sflip = (unsigned long long)(swap != neg) << 63;  // s = -1
+  const double st = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, t) ^ sflip);
+  const double stz = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, t * z) ^ sflip);
+  const double res = Ops::fma(stz, P, Ops::fma(1.0, st, C));  // C + s t is one rounding
+  score = umin(score, mid_score(res));
+  return res;
+}
+
+// (float)sin(x), (float)cos(x) for x an fp32 value in chunk_ok's domain
+// (|x| < 2^26, x != -0); folds both double results into score.
+template <class Ops>
+SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score) {
+  const double x = (double)xf;
+  const double kd = __builtin_rint(x * kTwoOverPi);
+  // x and kd*P1 are multiples of 2^-52 and |x - kd*P1| < 2, so r1 is exact
+  const double r1 = Ops::fma(-kd, kP1, x);
+  const double r = Ops::fma(-kd, kP2, r1);
+  const int q = (int)kd;
+  const double z = r * r;
+  const double z2 = z * z;
+  // sin r = r + r^3 (S1 + z S'(z)), S' = (S2 + S3 z) + z^2 ((S4 + S5 z) + z^2 S6)
+  const double sp = Ops::fma(z2, Ops::fma(kS6, z2, Ops::fma(kS5, z, kS4)), Ops::fma(kS3, z, kS2));
+  const double sr = Ops::fma(r * z, Ops::fma(z, sp, kS1), r);
+  // cos r = (1 - z/2) + z^2 C(z), C = (C1 + C2 z) + z^2 ((C3 + C4 z) + z^2 (C5 + C6 z));
+  // 1 - z/2 in one rounding (cos r >= 0.7: 1 ulp, no compensation needed)
+  const double cp = Ops::fma(z2, Ops::fma(z2, Ops::fma(kC6, z, kC5), Ops::fma(kC4, z, kC3)), Ops::fma(kC2, z, kC1));
+  const double cr = Ops::fma(z2, cp, Ops::fma(z, -0.5, 1.0));
+  score = umin(score, umin(mid_score(sr), mid_score(cr)));
+  // quadrant q mod 4: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s), on the
+  // rounded floats (rounding commutes with negation)
+  const float s32 = (float)sr, c32 = (float)cr;
+  const float sw = (q & 1) ? c32 : s32;
+  const float cw = (q & 1) ? s32 : c32;
+  sf = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, sw) ^ ((unsigned)q << 30 & 0x80000000u));
+  cf = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, cw) ^ ((unsigned)(q + 1) << 30 & 0x80000000u));
+}
+
+// The closing check of a chunk that ran the fast path from a chunk_ok state:
+// phaseEst, integrator and trigOffset finite and small enough for the next
+// chunk (trigOffset only grows; the feedback floats are sin / cos results of
+// arguments in the domain, so 0 or >= 2^-54 -- see chunk_ok).  A NaN
+// anywhere in the chunk reaches phaseEst, and fails here.
+SDR_HD inline bool chunk_end_ok(float integrator, float phaseEst, float trigOffset) {
+  return __builtin_fmaf(__builtin_fabsf(integrator), 16.0f, __builtin_fabsf(phaseEst)) + trigOffset < 0x1p24f;
+}
+
+}  // namespace pllfast
+}  // namespace sdr

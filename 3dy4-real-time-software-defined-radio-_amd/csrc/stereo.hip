@@ -15,6 +15,7 @@
 // arguments in double (the reference calls the double C functions), every
 // result rounded back to float where the reference stores a float.
 #include "sdr_common.hpp"
+#include "pll_fast.hpp"
 
 #pragma clang fp contract(off)
 
@@ -30,6 +31,15 @@ constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
 // not feed back, so this kernel only records trigArg (args[k+1] for sample k,
 // args[0] = the incoming nco_state) and nco_kernel evaluates all of them in
 // parallel.  The last sample's NCO becomes the new nco_state here.
+//
+// FAST: each step first runs the short-chain atan2 / sincos of pll_fast.hpp,
+// which certify that their float results are the reference's; a chunk of 8
+// steps in which any lane of the wave could not certify a result is run again
+// from its saved state with the library routines (a wave-uniform branch, off
+// the recurrence's chain).  The stored arguments of the first pass are
+// rewritten by the second, so every output is the library path's or a
+// certified equal.
+template <int FAST>
 __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, long long n, int nstreams,
                                                  long long in_stride, float freq, float Fs, float nco_scale,
                                                  float phase_adjust, float norm_bw, float* __restrict__ pll,
@@ -60,6 +70,25 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     fbI = (float)cv;
     fbQ = (float)sv;
   };
+  // the same step through pll_fast.hpp; score keeps the chunk's certificate
+  struct DevOps {
+    static __device__ double fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+    static __device__ double rcp(double u) { return __builtin_amdgcn_rcp(u); }
+  };
+  unsigned score = 0u;
+  auto fast_step = [&](float v) __attribute__((always_inline)) {
+    const float eI = (v == 0.0f ? 1.0f : v) * fbI;
+    const float eQ = v * (-1.0f * fbQ);
+    const float eD = pllfast::atan2_fast<DevOps>(eQ, eI, score);
+    integrator = integrator + Ki * eD;
+    phaseEst = phaseEst + (Kp * eD + integrator);
+    trigOffset = trigOffset + 1.0f;
+    arg = (float)(step * (double)trigOffset + (double)phaseEst);
+    pllfast::sincos_fast<DevOps>(arg, fbQ, fbI, score);
+  };
+  const bool gains_ok = __builtin_fabsf(Kp) <= 1.0f && __builtin_fabsf(Ki) <= 1.0f;  // chunk_ok's premise
+  // chunk_ok of the state a chunk starts from (the previous chunk's closing check)
+  bool start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
   // The chain is latency-bound (one lane per stream).  Inputs are loaded one
   // chunk ahead into registers, so no step waits on memory: a per-sample
   // load put a full load latency -- and the previous step's store, which
@@ -74,11 +103,29 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     __builtin_amdgcn_sched_barrier(0);
   };
   auto run = [&](const float (&buf)[CH], long long k0) __attribute__((always_inline)) {
+    if constexpr (FAST) {
+      const float s0 = fbI, s1 = fbQ, s2 = integrator, s3 = phaseEst, s4 = trigOffset;
+      score = start_ok ? ~0u : 0u;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        fast_step(buf[j]);
+        if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
+      }
+      start_ok = pllfast::chunk_end_ok(integrator, phaseEst, trigOffset);
+      // 2: timing experiment only (no re-run)
+      if (FAST == 2 || !__any(score < pllfast::kCertified || !start_ok)) return;
+      fbI = s0;
+      fbQ = s1;
+      integrator = s2;
+      phaseEst = s3;
+      trigOffset = s4;
+    }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       pll_step(buf[j]);
       if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
     }
+    if constexpr (FAST) start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
   };
   // ping-pong register chunks (no copies, so no wait at the chunk boundary
   // beyond the chunk being consumed); a chunk past nc re-loads an in-bounds one
@@ -136,8 +183,17 @@ __global__ __launch_bounds__(kWG) void stereo_pcm_kernel(const float* __restrict
 hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
                                  float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
                                  long long args_stride, hipStream_t st) {
-  hipLaunchKernelGGL(pll_kernel, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams, in_stride,
-                     freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+  // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests)
+  const int fast = env_int("SDR_PLL_FAST", 1);
+  if (fast == 2)
+    hipLaunchKernelGGL(pll_kernel<2>, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams,
+                       in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+  else if (fast)
+    hipLaunchKernelGGL(pll_kernel<1>, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams,
+                       in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+  else
+    hipLaunchKernelGGL(pll_kernel<0>, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams,
+                       in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
   return hipGetLastError();
 }
 

@@ -170,7 +170,10 @@ def cpu_baseline(seconds: float, config: str):
         return json.loads(out)
 
     one = run("frontend", block, seconds / 4, 1)
-    many = run("frontend", block, seconds / 2, 0)
+    share = run("frontend", block, seconds / 4, 0)
+    # SURVEY 8(d) asks for all host cores: one thread per CPU of the affinity
+    # set, even where the cgroup quota grants fewer (they then time-share)
+    many = run("frontend", block, seconds / 4, share["affinity"]) if share["affinity"] > share["threads"] else share
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -182,14 +185,16 @@ def cpu_baseline(seconds: float, config: str):
         pass
     rate = lambda d: d["pairs"] / d["seconds"] / 1e6  # noqa: E731
     res = {"value": round(rate(many), 2), "unit": "MS/s", "cores": many["threads"], "kind": kind,
-           "value_1core": round(rate(one), 2),
-           "sample": f"{one['pairs'] + many['pairs']} IQ pairs in {block:,}-pair mode-0 blocks (101-tap FIR+dec10 "
-                     f"on I and Q, then the discriminator: src/project.cpp:86-90), one independent stream per "
-                     f"std::thread on all {many['threads']} cores of this process's CPU share for {seconds / 2:.0f} s, "
-                     f"and 1 thread for {seconds / 4:.0f} s; host {model}",
-           "cpu_share": {"cores": many["threads"], "affinity": many["affinity"],
-                         "cgroup_quota": many["cgroup_quota"] or None,
-                         "omp_num_threads": many["omp_num_threads"] or None}}
+           "value_1core": round(rate(one), 2), "value_share": round(rate(share), 2),
+           "sample": f"{one['pairs'] + share['pairs'] + (many['pairs'] if many is not share else 0)} IQ pairs in "
+                     f"{block:,}-pair mode-0 blocks (101-tap FIR+dec10 on I and Q, then the discriminator: "
+                     f"src/project.cpp:86-90), one independent stream per std::thread: {many['threads']} threads "
+                     f"(every CPU of the affinity set) for {seconds / 4:.0f} s, {share['threads']} threads (the "
+                     f"CPU share: affinity capped by the cgroup quota) for {seconds / 4:.0f} s and 1 thread for "
+                     f"{seconds / 4:.0f} s; host {model}",
+           "cpu_share": {"cores": share["threads"], "affinity": share["affinity"],
+                         "cgroup_quota": share["cgroup_quota"] or None,
+                         "omp_num_threads": share["omp_num_threads"] or None}}
     proj = os.path.join(REPO, "oracle", "_ref", "project_ref")
     if kind == "reference" and os.path.exists(proj):
         # config 1: ~1 s of the single-process program, then one process per core

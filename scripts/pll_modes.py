@@ -1,0 +1,43 @@
+"""Time the fmPLL recurrence kernel per mode (SDR_PLL_FAST = 0 library
+routines, 1 certified short chain, 2 short chain without the re-run, timing
+only) on 1,024 streams x 5,120 samples, and count the samples where mode 2
+differs from mode 0.  usage: python scripts/pll_modes.py [trig0]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "3dy4-real-time-software-defined-radio-_amd"))
+import sdrhip  # noqa: E402
+
+trig0 = float(sys.argv[1]) if len(sys.argv) > 1 else 0.0
+ctx = sdrhip.Context(0)
+S, n, Fs = 1024, 5120, 240e3
+rng = np.random.default_rng(3)
+t = np.arange(n)
+x = (rng.uniform(0.01, 0.3, S)[:, None] * np.cos(2 * np.pi * (19e3 + rng.uniform(-40, 40, S)[:, None]) / Fs * t
+                                                 + rng.uniform(0, 6.3, S)[:, None])
+     + rng.normal(0, 0.01, (S, n))).astype(np.float32)
+A = sdrhip.DeviceArray
+d_x = A.from_numpy(ctx, x)
+st0 = np.tile(np.array([1, 0, 0, 0, trig0, 1], np.float32), S)
+outs = {}
+for mode in ("0", "1", "2", "1", "0"):
+    os.environ["SDR_PLL_FAST"] = mode
+    d_pll = A.from_numpy(ctx, st0)
+    d_out = A(ctx, S * n * 4)
+    ctx.fm_pll_dev(d_x, n, S, n, 19e3, Fs, 2.0, 0.0, 0.01, d_pll, None, n, d_out, n)  # warm
+    ctx.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.fm_pll_dev(d_x, n, S, n, 19e3, Fs, 2.0, 0.0, 0.01, d_pll, None, n, d_out, n)
+    ctx.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    outs[mode] = d_out.download()
+    print(f"mode {mode}: {ms:.3f} ms per call (recurrence + NCO), trig0 {trig0:g}", flush=True)
+diff = int(np.count_nonzero(outs["2"].view(np.uint32) != outs["0"].view(np.uint32)))
+same = bool(np.array_equal(outs["1"].view(np.uint32), outs["0"].view(np.uint32)))
+print(f"mode2 vs mode0 differing samples: {diff} of {outs['0'].size}; mode1 == mode0: {same}")

@@ -515,6 +515,42 @@ def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix, n):
             assert_bits(dev_st[s], ost[s], f"pll state stream {s} block {b}")
 
 
+@pytest.mark.parametrize("trig0", [0.0, 3.0e6, 1.6e7])
+def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
+    """The PLL kernel's certified short-chain path (csrc/pll_fast.hpp, the
+    default) against its library-routine path (SDR_PLL_FAST=0) on 512 streams
+    x 8,192 samples, bitwise, and 8 streams of it against the oracle.  trig0
+    starts the oscillator's trigOffset late (oscillator arguments up to ~8e6
+    rad: the reduction's large-argument range; 1.6e7 reaches fp32's integer
+    limit, where trigOffset++ stops advancing, src/filter.cpp:212)."""
+    sdrhip = built_lib
+    rng = np.random.default_rng(int(trig0) + 5)
+    S, n, Fs = 512, 8192, 240e3
+    t = np.arange(n)
+    f = 19e3 + rng.uniform(-40, 40, S)[:, None]
+    x = (rng.uniform(0.01, 0.3, S)[:, None] * np.cos(2 * np.pi * f / Fs * t + rng.uniform(0, 6.3, S)[:, None])
+         + rng.normal(0, 0.01, (S, n))).astype(np.float32)
+    x[:, ::1013] = 0.0
+    st0 = np.tile(np.array([1, 0, 0, 0, trig0, 1], np.float32), S)
+    A = sdrhip.DeviceArray
+    d_x = A.from_numpy(gpu_ctx, x)
+    res = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("SDR_PLL_FAST", fast)
+        d_pll = A.from_numpy(gpu_ctx, st0)
+        d_out = A(gpu_ctx, S * n * 4)
+        gpu_ctx.fm_pll_dev(d_x, n, S, n, 19e3, Fs, 2.0, 0.0, 0.01, d_pll, None, n, d_out, n)
+        gpu_ctx.synchronize()
+        res[fast] = (d_out.download().reshape(S, n), d_pll.download().reshape(S, 6))
+    assert_bits(res["1"][0], res["0"][0], "nco fast vs library")
+    assert_bits(res["1"][1], res["0"][1], "pll state fast vs library")
+    for s in range(0, S, 64):
+        ost = st0[6 * s:6 * s + 6].copy()
+        nco = oracle.fm_pll(x[s], 19e3, Fs, 2.0, 0.0, 0.01, ost)
+        assert_bits(res["1"][0][s], nco, f"stream {s} vs oracle")
+        assert_bits(res["1"][1][s], ost, f"stream {s} state vs oracle")
+
+
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                                              (147, 1280, 101, 100, 12800), (3, 5, 101, 100, 5000)])
 def test_resample_plan_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, n):

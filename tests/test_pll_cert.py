@@ -1,0 +1,40 @@
+"""CPU check of the PLL's certified short-chain transcendentals
+(csrc/pll_fast.hpp): wherever atan2_fast / sincos_fast certify a result, its
+float equals the reference's (float)atan2/sin/cos of the double library
+routines (src/filter.cpp:199, :216-217), and the kernel's chunk-and-rerun
+recurrence reproduces the reference recurrence bit for bit.  The host build
+is tests/pll_cert.cpp (g++, glibc as the reference's libm); the device runs
+the same header (tests/test_gpu_parity.py::test_pll_fast_vs_library)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "3dy4-real-time-software-defined-radio-_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def cert_bin(tmp_path_factory):
+    out = tmp_path_factory.mktemp("pllcert") / "pll_cert"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", str(out),
+                    os.path.join(ROOT, "tests", "pll_cert.cpp")], check=True)
+    return str(out)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_pll_fast_certificate(cert_bin, seed):
+    r = json.loads(subprocess.run([cert_bin, "2000000", str(seed)], check=True, capture_output=True,
+                                  text=True).stdout)
+    for k in ("atan2", "sincos", "sincos_worst"):
+        n, certified, mismatch = r[k]
+        assert mismatch == 0, (k, r)
+        assert certified > 0.9 * n, (k, r)  # the fast path is the common path
+    assert r["atan2_special"] == 0, r
+    assert r["atan2_max_rel_log2"] < -45.5, r  # the fit's 2^-46.8 plus rounding, far inside the 2^-40 margin  # no subnormal / NaN errorD off x = y = 0 in the kernel's domain
+    assert r["pll_mismatch"] == 0, r
+    # re-run chunks are rare (8 steps each)
+    assert r["pll_chunks_rerun"] * 8 < 0.01 * r["pll_steps"], r
