@@ -184,8 +184,13 @@ def cpu_baseline(seconds: float, config: str):
     except OSError:
         pass
     rate = lambda d: d["pairs"] / d["seconds"] / 1e6  # noqa: E731
-    res = {"value": round(rate(many), 2), "unit": "MS/s", "cores": many["threads"], "kind": kind,
+    # the headline is the faster of the two all-core runs: on a box whose
+    # cgroup quota grants fewer CPUs than its affinity set, one thread per
+    # affinity CPU time-shares the quota and runs slower than the share
+    best = many if rate(many) >= rate(share) else share
+    res = {"value": round(rate(best), 2), "unit": "MS/s", "cores": best["threads"], "kind": kind,
            "value_1core": round(rate(one), 2), "value_share": round(rate(share), 2),
+           "value_affinity": round(rate(many), 2), "threads_affinity": many["threads"],
            "sample": f"{one['pairs'] + share['pairs'] + (many['pairs'] if many is not share else 0)} IQ pairs in "
                      f"{block:,}-pair mode-0 blocks (101-tap FIR+dec10 on I and Q, then the discriminator: "
                      f"src/project.cpp:86-90), one independent stream per std::thread: {many['threads']} threads "
