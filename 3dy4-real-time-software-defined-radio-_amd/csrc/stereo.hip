@@ -106,10 +106,12 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     if constexpr (FAST) {
       const float s0 = fbI, s1 = fbQ, s2 = integrator, s3 = phaseEst, s4 = trigOffset;
       score = start_ok ? ~0u : 0u;
+      // unconditional: args rows hold n + 1 floats (launch_pll_recurrence), so
+      // ar[n] is the row's spare slot -- no per-step bounds compare and branch
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         fast_step(buf[j]);
-        if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
+        ar[k0 + j + 1] = arg;
       }
       start_ok = pllfast::chunk_end_ok(integrator, phaseEst, trigOffset);
       // 2: timing experiment only (no re-run)
@@ -180,9 +182,12 @@ __global__ __launch_bounds__(kWG) void stereo_pcm_kernel(const float* __restrict
 
 }  // namespace
 
+// args: [nstreams][args_stride] with args_stride >= n + 1 (args[s][n] is
+// written, a spare slot: the kernel stores every step's argument unguarded)
 hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
                                  float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
                                  long long args_stride, hipStream_t st) {
+  if (args_stride < n + 1) return hipErrorInvalidValue;
   // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests)
   const int fast = env_int("SDR_PLL_FAST", 1);
   if (fast == 2)
