@@ -19,8 +19,8 @@
 //     ds_read_b128 chunks (lane stride D*R dwords, 20 for D=10 R=2:
 //     conflict-free) and keeps all R outputs of I and Q in registers; the
 //     taps are SGPR operands of the multiplies, loaded once per pass over a
-//     third of the taps (TM 1, default), or per-output LDS rows read as
-//     wave-wide broadcasts (TM 0);
+//     third of the taps (an earlier LDS tap-row mode for D = 1 lost its A/B:
+//     31.4 vs 37.8 us per 1,024 x 5,120 block, scripts/d1bench.py);
 //   * fused launches apply the discriminator in registers and write only the
 //     demodulated stream: decimated I/Q never touch HBM.  Lane 0 of each wave
 //     re-derives the R outputs before its span (E = R) so waves never wait on
@@ -95,22 +95,18 @@ struct Geom {
   static constexpr int HALO = (T - 1 + 3) / 4 * 4;                 // (T-1) rounded up to a float4
   static constexpr int SPAN = HALO + D * (R - 1) + 1;              // positions one lane reads
   static constexpr int NCHUNK = (SPAN + 3) / 4;                    // float4 chunks per lane window
-  static constexpr int SPAN4 = 4 * NCHUNK;                         // tap row length
-  // tap-row reuse: rows GR apart are offset by D*GR taps = SH whole chunks
-  static constexpr int GQ = (D % 4 == 0) ? 1 : (D % 2 == 0) ? 2 : 4;
-  static constexpr int GR = GQ < R ? GQ : R;                       // tap rows read from LDS per chunk
-  static constexpr int SH = D * GR / 4;                            // chunk shift between reused rows
+  static constexpr int SPAN4 = 4 * NCHUNK;                         // a lane window, whole chunks
   static constexpr int LDS_LEN = D * ((NW - 1) * WADV + 63 * R) + SPAN4;  // floats per channel
   static constexpr int LDS4 = LDS_LEN / 4;
   static constexpr int FULL = LDS4 / NTH, REM = LDS4 % NTH;        // staging rows per thread
   // the block's last STRIP inputs per channel, staged by tile 0: the
   // prev_* recompute (D+T-1 inputs) and the new state (ns <= STRIP)
   static constexpr int STRIP = ((D + T - 1 > 128 ? D + T - 1 : 128) + 3) / 4 * 4;
-  // LDS floats: channels, tap rows, two tail strips
+  // LDS floats: the channels (the two tail strips reuse them)
   // (the strips reuse the channel buffers after tile 0's scan: LDS per
   // wave sets the occupancy, 13 -> 14 one-wave workgroups per CU at D = 10)
   static_assert(STRIP <= LDS_LEN, "strip staged into the channel buffers");
-  static constexpr int SMEM = 2 * LDS_LEN + R * SPAN4;
+  static constexpr int SMEM = 2 * LDS_LEN;
 };
 
 __device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp) {
@@ -342,9 +338,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// TM = where the taps live: 0 LDS broadcast rows (D = 1), 1 SGPRs (NPASS
-// passes).  The loads of tile i+1 are issued into registers before tile i is
-// computed (prefetch depth 1).
+// TM = where the taps live: 1 SGPRs (NPASS passes), the only mode built.
+// The loads of tile i+1 are issued into registers before tile i is computed
+// (prefetch depth 1).
 // FMA = the fused multiply-add arithmetic mode (SDR_ARITH_FMA, SGPR taps
 // only): same taps, same order, one rounding per tap instead of two -- not
 // the reference's bits, within the fp32 tolerance of DESIGN.md 2.
@@ -354,12 +350,11 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   constexpr int NTH = G::NTH;
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
   static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
-  static_assert(!FMA || TM == 1, "FMA mode: SGPR taps");
+  static_assert(TM == 1, "taps as SGPR operands");
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lds0 = smem;
   float* lds1 = smem + G::LDS_LEN;
-  float* htab = smem + 2 * G::LDS_LEN;  // R tap rows (TM 0)
   float* strip0 = lds0;                 // the block's last inputs (tile 0, after its scan)
   float* strip1 = lds1;
 
@@ -389,16 +384,6 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     last = min((x + 1) * per_xcd, total);
   }
   if (first >= last) return;
-
-  // tap rows, once per workgroup: htab[r][w] = h[HALO + D*r - w] (0 where
-  // that k is not a tap)
-  if constexpr (TM == 0) {
-    for (int i = tid; i < R * G::SPAN4; i += NTH) {
-      const int r = i / G::SPAN4, w = i - r * G::SPAN4;
-      const int k = G::HALO + D * r - w;
-      htab[i] = (k >= 0 && k < T) ? h[k] : 0.0f;
-    }
-  }
 
   using Stage = float4[G::FULL + 1];
   Stage sa0, sa1;
@@ -442,15 +427,9 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
     // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
-    // 4-position chunk c it reads NCH input float4s (its own window) and the
-    // taps of the top GR output rows (one address for the whole wave: an LDS
-    // broadcast).  Output row r < R-GR applies, at chunk c, exactly the taps
-    // row r+GR applied at chunk c+SH (D*GR is a multiple of 4), so those
-    // come from registers loaded SH chunks earlier: at R = 4, D = 10 half
-    // the tap reads disappear.  The next chunk is prefetched; the
-    // sched_barrier keeps the scheduler from hoisting every LDS read of the
-    // unrolled loop (registers -> occupancy).
-    constexpr int GR = G::GR, SH = G::SH, C0 = G::NCHUNK - 1;
+    // 4-position chunk c it reads NCH input float4s of its own window; the
+    // next chunk is prefetched, and the sched_barrier keeps the scheduler from
+    // hoisting every LDS read of the unrolled loop (registers -> occupancy).
     const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
     float acc0[R], acc1[R];
 #pragma unroll
@@ -464,52 +443,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
-      if constexpr (TM == 0) {
-        const float* ht = htab + (R - GR) * G::SPAN4;  // the top GR rows
-        float4 top[G::NCHUNK][GR];                     // compile-time indexed: SSA values
-        float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * C0);
-        float4 q1 = q0;
-        if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * C0);
-#pragma unroll
-        for (int g = 0; g < GR; ++g) top[C0][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * C0);
-#pragma unroll
-        for (int c = C0; c >= 0; --c) {
-          float4 n0 = q0, n1 = q1;
-          if (c > 0) {
-            n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
-            if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
-#pragma unroll
-            for (int g = 0; g < GR; ++g)
-              top[c - 1][g] = *reinterpret_cast<const float4*>(ht + g * G::SPAN4 + 4 * (c - 1));
-          }
-          const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
-          const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-          for (int j = 3; j >= 0; --j) {
-            const int w = 4 * c + j;  // window position; output r sits at HALO + D*r
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-              const int k = G::HALO + D * r - w;
-              if (k >= 0 && k < T) {
-                // row r at chunk c == top row r + m*GR at chunk c + m*SH
-                const int m = r >= R - GR ? 0 : (R - GR - r + GR - 1) / GR;
-                const float4 hv = top[c + m * SH][r + m * GR - (R - GR)];
-                const float hk = j == 0 ? hv.x : j == 1 ? hv.y : j == 2 ? hv.z : hv.w;
-                acc0[r] = acc0[r] + hk * e0[j];
-                if (NCH == 2) acc1[r] = acc1[r] + hk * e1[j];
-              }
-            }
-          }
-          q0 = n0;
-          q1 = n1;
-          // Pin both channels' chains to this chunk: without it LLVM defers
-          // one channel's products past later chunks (holding their operands
-          // live -> 256 VGPRs at R = 4).
-#pragma unroll
-          for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
+      {
         // Taps as SGPR operands of the multiplies: no LDS tap traffic.  All
         // T taps do not fit the SGPR file beside the addressing, so the
         // window is walked in NPASS passes over consecutive tap ranges
@@ -805,14 +739,14 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
   }
   static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
   a.ablate = ablate;
-  const size_t lds = (size_t)(G::SMEM - (TM == 1 ? R * G::SPAN4 : 0)) * sizeof(float);  // TM 1: no tap rows
+  const size_t lds = (size_t)G::SMEM * sizeof(float);
   hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st,
                      a, h);
   return hipGetLastError();
 }
 
 // Tile shape per decimation factor: R outputs per lane, one wave per
-// workgroup, taps in SGPRs (TM 1) or LDS rows (TM 0), waves per CU.  D*R must
+// workgroup, taps in SGPRs (TM 1), waves per CU.  D*R must
 // be a multiple of 4 (aligned lane windows).  These are the measured best on
 // MI355X (where the variants that lost are listed).
 struct Variant {
@@ -824,7 +758,9 @@ Variant variant_for(int D, bool demod, Src src) {
     // f32 fused: 64 one-wave workgroups per CU
     case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 64} : Variant{2, 1, 1, 32};
     case 5: return {4, 1, 1, 32};
-    case 1: return {4, 1, 0, 32};
+    // D = 1 (the band-pass filters): SGPR taps too -- 31.4 vs 37.8 us per
+    // 1,024 x 5,120 block against LDS tap rows (scripts/d1bench.py)
+    case 1: return {4, 1, 1, 32};
     default: return {0, 0, 0, 32};
   }
 }
@@ -860,7 +796,7 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
       switch (a.D) {
         case 10: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         case 5: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 1: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC, 0>(a, h, st, v.wpc);
+        case 1: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         default: break;
       }
     }
