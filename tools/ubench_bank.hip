@@ -2,7 +2,7 @@
 // for v_add_f32 / v_mul_f32 whose two VGPR sources sit in the same register
 // bank (index mod 4) or in different banks, W waves per SIMD, every CU busy.
 // Destinations rotate over 8 registers, so no instruction depends on the one
-// before it.  Build: hipcc --offload-arch=gfx950 -O3 tools/ubench_bank.hip
+// before it.  Build: python3 scripts/gen_ubench_scan.py && hipcc --offload-arch=gfx950 -O3 -Itools tools/ubench_bank.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
