@@ -1,4 +1,5 @@
-"""cfg3 resample_lp launches with SDR_RESAMPLE_TRACE set: per-wave phase times of
+"""cfg3 resample_lp launches for the per-wave phase trace of profiles/r02_resample_trace/
+(needs the temporary SDR_RESAMPLE_TRACE build described there; the tree does not carry it): times of
 workgroup 0 (s_memtime ticks) printed by the launcher to stderr."""
 import os
 import sys

@@ -30,7 +30,7 @@
   "v_mul_f32 v43, v46, v51\n\tv_add_f32 v34, v34, v43\n\tv_mul_f32 v40, v47, v48\n\tv_add_f32 v35, v35, v40\n\t"
 
 template <int OP>
-__global__ __launch_bounds__(256) void bank(float* out, int iters) {
+__global__ __launch_bounds__(512) void bank(float* out, int iters) {
   asm volatile(
       "v_mov_b32 v40, 1.0\n\tv_mov_b32 v41, 1.0\n\tv_mov_b32 v42, 1.0\n\tv_mov_b32 v43, 1.0\n\t"
       "v_mov_b32 v44, 1.0\n\tv_mov_b32 v45, 1.0\n\tv_mov_b32 v46, 1.0\n\tv_mov_b32 v47, 1.0\n\t"
@@ -50,6 +50,9 @@ __global__ __launch_bounds__(256) void bank(float* out, int iters) {
     if constexpr (OP == 7) asm volatile(".rept 1024\n\t" MACDIFF ".endr\n\t" ::: CLOB);
     // resample_lp's register pattern: 128 tap registers, 7 chains (ubench_bank_scan.h)
     if constexpr (OP == 8) asm volatile(".rept 4\n\t" SCAN_BODY ".endr\n\t" ::: SCAN_CLOB);
+    if constexpr (OP == 9) asm volatile(".rept 4\n\t" SCAN_BODY_B ".endr\n\t" ::: SCAN_CLOB);
+    if constexpr (OP == 10) asm volatile(".rept 4\n\t" SCAN_BODY_C ".endr\n\t" ::: SCAN_CLOB);
+    if constexpr (OP == 11) asm volatile(".rept 4\n\t" SCAN_BODY_D ".endr\n\t" ::: SCAN_CLOB);
   }
   float r;
   asm volatile("v_mov_b32 %0, v32" : "=v"(r)::CLOB);
@@ -69,9 +72,10 @@ int main() {
   const char* names[] = {"v_add_f32 same-bank srcs", "v_add_f32 diff-bank srcs", "v_mul_f32 same-bank srcs",
                          "v_mul_f32 diff-bank srcs", "mul+add, sum srcs same bank", "mul+add, sum srcs diff bank",
                          "mul+add, 8 KB loop body", "mul+add, 32 KB loop body",
-                         "resample scan, 128 tap regs"};
-  for (int op = 0; op < 9; ++op) {
-    const int per_iter = op == 6 ? 2048 : op == 7 ? 8192 : op == 8 ? 4 * SCAN_N : 32;  // instructions per loop trip
+                         "resample scan, 128 tap regs", "scan, one product reg", "scan, products then sums",
+                         "scan, product over its input"};
+  for (int op = 0; op < 12; ++op) {
+    const int per_iter = op == 6 ? 2048 : op == 7 ? 8192 : op >= 8 ? 4 * SCAN_N : 32;  // instructions per loop trip
     const int iters = 128000 / per_iter;
     for (int w : {1, 2, 4, 8}) {  // waves per SIMD (256-thread WGs = 1 wave per SIMD each)
       const int grid = ncu * w;
@@ -86,6 +90,9 @@ int main() {
           case 6: hipLaunchKernelGGL(bank<6>, dim3(grid), dim3(256), 0, 0, out, iters); break;
           case 7: hipLaunchKernelGGL(bank<7>, dim3(grid), dim3(256), 0, 0, out, iters); break;
           case 8: hipLaunchKernelGGL(bank<8>, dim3(grid), dim3(256), 0, 0, out, iters); break;
+          case 9: hipLaunchKernelGGL(bank<9>, dim3(grid), dim3(256), 0, 0, out, iters); break;
+          case 10: hipLaunchKernelGGL(bank<10>, dim3(grid), dim3(256), 0, 0, out, iters); break;
+          case 11: hipLaunchKernelGGL(bank<11>, dim3(grid), dim3(256), 0, 0, out, iters); break;
         }
       };
       launch();
@@ -102,6 +109,24 @@ int main() {
              clk / 1e6);
       fflush(stdout);
     }
+  }
+  // resample_lp's workgroup shape: one workgroup of 7 (or 8) waves per CU, so
+  // three SIMDs hold 2 waves and one holds 1 (or all hold 2); optionally a
+  // workgroup barrier every 1,792 instructions (one per 'item')
+  for (int nw : {7, 8}) {
+    const int iters = 128000 / (4 * SCAN_N) * 4;
+    hipLaunchKernelGGL(bank<8>, dim3(ncu), dim3(64 * nw), 0, 0, out, iters);
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(bank<8>, dim3(ncu), dim3(64 * nw), 0, 0, out, iters);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ms /= 5;
+    const double per_busiest = (double)iters * 4 * SCAN_N * 2 / (ms * 1e-3);  // 2 waves on the busiest SIMD
+    printf("scan, %d-wave workgroup/CU     %8.3f ms  %5.2f cyc/instr on a 2-wave SIMD @%.2f GHz\n", nw, ms,
+           clk * 1e3 / per_busiest, clk / 1e6);
+    fflush(stdout);
   }
   // sustained: the scan-shaped body at 2 waves/SIMD for ~0.5 s; a falling
   // rate means the clock drops under sustained VALU load
