@@ -495,6 +495,10 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  // The next item's DMAs (issued before this scan) are waited for here,
+  // before the output stores: vmcnt also counts stores, so a drain after them
+  // would wait out their write latency too.
+  dma_drain();
   float* ys = a.y + (long long)st * a.y_stride;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -535,7 +539,8 @@ __global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
     tp[u + 3] = v.w;
   }
   for (int it = i0; it < i1; ++it) {
-    dma_drain();
+    // (the previous item drained its DMAs before its output stores)
+    if (it == i0 || a.ablate == 2) dma_drain();
     __syncthreads();  // item it's span has landed; the other buffer is free
     // the stream's first item is the only reader of its old state and its span
     // is staged now: state <- last ns inputs of the block (src/filter.cpp:169),
