@@ -52,6 +52,9 @@ sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 FP32_VALU_PEAK_TFLOPS = 157.3
+# discriminator per decimated output (src/filter.cpp:88-98): I*I + Q*Q (3), the two
+# differences and products (4), a - b and the divide (2)
+DEMOD_FLOP = 9.0
 
 CONFIGS = {
     # name: (kind, D or (up, down), ntaps, pairs per stream per step, streams per GPU)
@@ -291,7 +294,7 @@ class Job:
             self.units = S * n
             self.bytes_per_pair = 2.0 + 2.0 * na / n  # u8 IQ in, s16 PCM out (intermediates are algorithmically free)
             # FIR MACs at 2 FLOP each (front end, audio LPF at the IF rate / 5) + the discriminator
-            self.flops_per_unit = 2 * 2 * T / D + 2.0 * 101 / (D * down) + 1.0 / D
+            self.flops_per_unit = 2 * 2 * T / D + 2.0 * 101 / (D * down) + DEMOD_FLOP / D
             self.metric = "IQ MSamples/sec through the mode-0 mono path (u8 IQ -> s16 PCM)"
             self.bound = "valu"
         elif kind == "stereo_u8":
@@ -313,7 +316,7 @@ class Job:
             self.units = S * n
             self.bytes_per_pair = 2.0 + 4.0 * na / n
             # front end + mono and stereo audio LPFs (IF/5 rate) + pilot and stereo BPFs (IF rate)
-            self.flops_per_unit = 2 * 2 * T / D + 2 * 2.0 * 101 / (D * down) + 2 * 2.0 * 101 / D + 1.0 / D
+            self.flops_per_unit = 2 * 2 * T / D + 2 * 2.0 * 101 / (D * down) + 2 * 2.0 * 101 / D + DEMOD_FLOP / D
             self.metric = "IQ MSamples/sec through the mode-0 stereo path (u8 IQ -> interleaved s16 L/R PCM)"
             self.bound = "valu"
         elif kind in ("frontend_f32", "frontend_u8"):
@@ -332,8 +335,8 @@ class Job:
                                                                    out, nout))
                 self.bytes_per_pair = 2.0 + 4.0 / D
             self.units = S * n  # IQ pairs per step
-            # 2 channels x T/D MACs x 2 FLOP, + the discriminator (~10 FLOP per decimated output)
-            self.flops_per_unit = 2 * 2 * T / D + 10.0 / D
+            # 2 channels x T/D MACs x 2 FLOP, + the discriminator per decimated output
+            self.flops_per_unit = 2 * 2 * T / D + DEMOD_FLOP / D
             self.metric = "IQ MSamples/sec through FIR+decimate+FM-demod"
             # f32 planar input: 8.4 B against ~41 FLOP per pair -> HBM-bound; the u8
             # wire format moves 2.4 B per pair, which puts the exact (no-FMA) FIR
