@@ -144,10 +144,20 @@ SDR_HD inline double atan2_abs(float y, float x, unsigned& score) {
   return res;
 }
 
+// The oscillator a fast step hands the next step's phase detector: the
+// reduced argument r (trigArg = r + q pi/2 + ~2^-84 |q|) and the double
+// sine S and cosine C of trigArg (the quadrant applied to fdlibm's kernels
+// of r), from which atan2_rot rotates.
+struct Osc {
+  double r, S, C;
+  int q;
+};
+
 // (float)sin(x), (float)cos(x) for x an fp32 value in chunk_ok's domain
-// (|x| < 2^26, x != -0); folds both double results into score.
+// (|x| < 2^26, x != -0); folds both double results into score and leaves
+// the oscillator in o.
 template <class Ops>
-SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score) {
+SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score, Osc& o) {
   const double x = (double)xf;
   const double kd = __builtin_rint(x * kTwoOverPi);
   // x and kd*P1 are multiples of 2^-52 and |x - kd*P1| < 2, so r1 is exact
@@ -164,13 +174,67 @@ SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score) 
   const double cp = Ops::fma(z2, Ops::fma(z2, Ops::fma(kC6, z, kC5), Ops::fma(kC4, z, kC3)), Ops::fma(kC2, z, kC1));
   const double cr = Ops::fma(z2, cp, Ops::fma(z, -0.5, 1.0));
   score = umin(score, umin(mid_score(sr), mid_score(cr)));
-  // quadrant q mod 4: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s), on the
-  // rounded floats (rounding commutes with negation)
-  const float s32 = (float)sr, c32 = (float)cr;
-  const float sw = (q & 1) ? c32 : s32;
-  const float cw = (q & 1) ? s32 : c32;
-  sf = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, sw) ^ ((unsigned)q << 30 & 0x80000000u));
-  cf = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, cw) ^ ((unsigned)(q + 1) << 30 & 0x80000000u));
+  // quadrant q mod 4: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s), applied
+  // to the doubles (kept for atan2_rot) and then rounded (rounding commutes
+  // with negation, so the floats are those of the rounded kernels)
+  const double sw = (q & 1) ? cr : sr;
+  const double cw = (q & 1) ? sr : cr;
+  o.S = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, sw) ^
+                                       ((unsigned long long)((unsigned)q << 30 & 0x80000000u) << 32));
+  o.C = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, cw) ^
+                                       ((unsigned long long)((unsigned)(q + 1) << 30 & 0x80000000u) << 32));
+  o.r = r;
+  o.q = q;
+  sf = (float)o.S;
+  cf = (float)o.C;
+}
+template <class Ops>
+SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score) {
+  Osc o;
+  sincos_fast<Ops>(xf, sf, cf, score, o);
+}
+
+// (float)atan2(y, x) for the phase detector of the step after the one that
+// left oscillator o: y = v * -fbQ, x = v' * fbI with fbI, fbQ the float
+// cos / sin of o's angle theta (v' = v for v != 0).  Instead of an atan
+// polynomial, (x, y) is rotated back by the known angle
+//   beta = -theta (+ pi for v < 0) = k pi/2 - r,  k in {-2, ..., 2}, beta in (-pi, pi]
+// (cos, sin of beta are +-(C, -S) of o): the residual angle is
+//   delta = atan((y C + x S) / (x C - y S)),  C, S = cos, sin theta,
+// which only the float roundings of fbI, fbQ, x and y make nonzero:
+// |delta| <= 2^-22 |sin theta cos theta| <= 2^-22 |beta|, so atan(t) = t
+// (t^3/3 is < 2^-66 |beta|) and v_rcp_f64's 2^-24.4 costs < 2^-46 |beta|;
+// the numerator's one rounding costs 2^-53 |S C|.  So the result
+// beta + delta is within ~2^-45 |result| of the exact atan2 -- as tight as
+// the polynomial's -- in ~12 double operations instead of ~27.  y = 0 (v = 0,
+// where x = fbI is a different geometry, or fbQ = 0) takes atan2's exact
+// values on the axis, +-0 or +-pi (x != 0 here: fbI is never 0).  Not
+// certified (score 0, the chunk re-runs): a result that rounds to +-pi_f
+// (beta + delta may have crossed +-pi, where atan2 wraps).
+template <class Ops>
+SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned& score) {
+  const int q4 = o.q & 3;
+  const double S = o.S, C = o.C;
+  const double X = (double)x, Y = (double)y;
+  const double num = Ops::fma(Y, C, X * S);
+  const double den = Ops::fma(X, C, -(Y * S));
+  const double d = num * Ops::rcp(den);
+  // k = (2 [v < 0] - q4) mod 4 as a representative in (-pi, pi]
+  int k = ((v < 0.0f ? 2 : 0) - q4) & 3;
+  k = k == 3 ? -1 : k;
+  k = (k == 2 && __builtin_signbit(o.r)) ? -2 : k;
+  const double kd = (double)k;
+  const double res = Ops::fma(kd, kP1, -o.r) + Ops::fma(kd, kP2, d);
+  const float f = (float)res;
+  const bool axis = y == 0.0f;
+  // atan2(+-0, x) = +-0 for x > 0, +-pi (rounded: pi_f) for x < 0
+  const float fa = x > 0.0f ? y : __builtin_copysignf(0x1.921fb6p+1f, y);
+  // branch-free: umin(score, mid) on the rotation's result, 0 if it rounds to
+  // +-pi_f, unchanged on the axis
+  const unsigned in_pi = 0u - (unsigned)(__builtin_fabsf(f) < 0x1.921fb6p+1f);
+  const unsigned cand = umin(score, mid_score(res)) & in_pi;
+  score = axis ? score : cand;
+  return axis ? fa : f;
 }
 
 // The closing check of a chunk that ran the fast path from a chunk_ok state:

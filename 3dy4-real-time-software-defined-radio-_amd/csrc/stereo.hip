@@ -14,6 +14,8 @@
 // fp32, atan2 / cos / sin of the fp32
 // arguments in double (the reference calls the double C functions), every
 // result rounded back to float where the reference stores a float.
+#include <type_traits>
+
 #include "sdr_common.hpp"
 #include "pll_fast.hpp"
 
@@ -76,16 +78,25 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     static __device__ double rcp(double u) { return __builtin_amdgcn_rcp(u); }
   };
   unsigned score = 0u;
-  auto fast_step = [&](float v) __attribute__((always_inline)) {
+  // the oscillator the previous fast step left: a chunk's steps 2..8 rotate
+  // back from it (pllfast::atan2_rot) instead of evaluating atan2
+  pllfast::Osc osc{0.0, 0.0, 1.0, 0};
+  auto fast_step = [&](float v, auto rot) __attribute__((always_inline)) {
     const float eI = (v == 0.0f ? 1.0f : v) * fbI;
     const float eQ = v * (-1.0f * fbQ);
-    const float eD = pllfast::atan2_fast<DevOps>(eQ, eI, score);
+    float eD;
+    if constexpr (decltype(rot)::value)
+      eD = pllfast::atan2_rot<DevOps>(eQ, eI, v, osc, score);
+    else
+      eD = pllfast::atan2_fast<DevOps>(eQ, eI, score);
     integrator = integrator + Ki * eD;
     phaseEst = phaseEst + (Kp * eD + integrator);
     trigOffset = trigOffset + 1.0f;
     arg = (float)(step * (double)trigOffset + (double)phaseEst);
-    pllfast::sincos_fast<DevOps>(arg, fbQ, fbI, score);
+    pllfast::sincos_fast<DevOps>(arg, fbQ, fbI, score, osc);
   };
+  using rot_t = std::true_type;
+  using poly_t = std::false_type;
   const bool gains_ok = __builtin_fabsf(Kp) <= 1.0f && __builtin_fabsf(Ki) <= 1.0f;  // chunk_ok's premise
   // chunk_ok of the state a chunk starts from (the previous chunk's closing check)
   bool start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
@@ -108,9 +119,13 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
       score = start_ok ? ~0u : 0u;
       // unconditional: args rows hold n + 1 floats (launch_pll_recurrence), so
       // ar[n] is the row's spare slot -- no per-step bounds compare and branch
+      // step 1 on the polynomial (a rotating first step after fast chunks,
+      // behind a wave-uniform branch, measured 1 % slower)
+      fast_step(buf[0], poly_t{});
+      ar[k0 + 1] = arg;
 #pragma unroll
-      for (int j = 0; j < CH; ++j) {
-        fast_step(buf[j]);
+      for (int j = 1; j < CH; ++j) {
+        fast_step(buf[j], rot_t{});
         ar[k0 + j + 1] = arg;
       }
       start_ok = pllfast::chunk_end_ok(integrator, phaseEst, trigOffset);

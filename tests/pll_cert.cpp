@@ -85,6 +85,31 @@ static void check_sincos(float x, Counts& c) {
   }
 }
 
+// atan2_rot: the phase detector of the step after sincos_fast(arg) -- y =
+// v * -fbQ, x = v' * fbI from that step's floats -- against glibc's atan2 of
+// the same floats (the kernel's steps 2..8 of a chunk)
+static void check_atan2_rot(float arg, float v, Counts& c) {
+  unsigned sc = ~0u;
+  float fbQ, fbI;
+  Osc o;
+  sincos_fast<HostOps>(arg, fbQ, fbI, sc, o);
+  const float eI = (v == 0.0f ? 1.0f : v) * fbI;
+  const float eQ = v * (-1.0f * fbQ);
+  unsigned score = ~0u;
+  const float eD = atan2_rot<HostOps>(eQ, eI, v, o, score);
+  const double refd = std::atan2((double)eQ, (double)eI);
+  const float ref = (float)refd;
+  ++c.n;
+  if (float_special(eD)) ++c.special;
+  if (score < kCertified) return;
+  ++c.certified;
+  if (fbits(eD) != fbits(ref)) {
+    if (c.mismatch < 5)
+      std::fprintf(stderr, "atan2_rot mismatch arg=%a v=%a fast=%a ref=%a\n", arg, v, (double)eD, (double)ref);
+    ++c.mismatch;
+  }
+}
+
 // src/filter.cpp:174-228's recurrence, the reference's way and the kernel's
 // way (chunks of 8 fast steps, a chunk re-run with the library routines when
 // any step was not certified; here one "wave" = one stream).  States and
@@ -100,6 +125,7 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
   r.trig = f.trig = trig0;
   long long bad_args = 0;
   bool start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig);
+  Osc osc{};  // the kernel's: a chunk's steps 2..8 rotate back from the previous step's oscillator
   auto lib_step = [&](Pll& p, float v) {
     const float eI = (v == 0.0f ? 1.0f : v) * p.fbI;
     const float eQ = v * (-1.0f * p.fbQ);
@@ -122,12 +148,12 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
       const float v = in[k0 + j];
       const float eI = (v == 0.0f ? 1.0f : v) * f.fbI;
       const float eQ = v * (-1.0f * f.fbQ);
-      const float eD = atan2_fast<HostOps>(eQ, eI, score);
+      const float eD = j > 0 ? atan2_rot<HostOps>(eQ, eI, v, osc, score) : atan2_fast<HostOps>(eQ, eI, score);
       f.integ = f.integ + Ki * eD;
       f.phase = f.phase + (Kp * eD + f.integ);
       f.trig = f.trig + 1.0f;
       fa[j] = (float)(step * (double)f.trig + (double)f.phase);
-      sincos_fast<HostOps>(fa[j], f.fbQ, f.fbI, score);
+      sincos_fast<HostOps>(fa[j], f.fbQ, f.fbI, score, osc);
     }
     start_ok = chunk_end_ok(f.integ, f.phase, f.trig);
     const bool bad = score < kCertified || !start_ok;
@@ -150,7 +176,7 @@ int main(int argc, char** argv) {
   std::mt19937_64 g(seed);
   std::uniform_real_distribution<double> U(-1.0, 1.0), E(-60.0, 60.0);
   std::bernoulli_distribution coin(0.5), rare(0.001);
-  Counts at, sc, scw;
+  Counts at, sc, scw, ar;
   auto logu = [&](double lo, double hi) {
     std::uniform_real_distribution<double> L(lo, hi);
     return (coin(g) ? -1.0 : 1.0) * std::exp2(L(g));
@@ -178,6 +204,9 @@ int main(int argc, char** argv) {
     }
     if (rare(g)) a = 0.0f;
     check_sincos(a, sc);
+    // the rotation: pilot-sized and whole-domain v (and exact zeros)
+    const float v = rare(g) ? 0.0f : (i % 2 ? (float)(0.3 * U(g)) : (float)logu(-60, 60));
+    check_atan2_rot(a, v, ar);
   }
   // the floats nearest to multiples of pi/2 (and their neighbours): the
   // reduction's hardest arguments (tiny reduced values)
@@ -188,6 +217,10 @@ int main(int argc, char** argv) {
     check_sincos(c, scw);
     check_sincos(std::nextafter(c, 1e30f), scw);
     check_sincos(std::nextafter(c, -1e30f), scw);
+    // tiny reduced arguments: beta near 0 or +-pi (the rotation's hardest)
+    const float v = (float)(0.3 * U(g));
+    check_atan2_rot(c, v, ar);
+    check_atan2_rot(std::nextafter(c, 1e30f), -v, ar);
   }
   // whole recurrences: noisy 19 kHz pilots, exact zeros, a large trigOffset start
   long long pll_bad = 0, reruns = 0, steps = 0;
@@ -205,9 +238,9 @@ int main(int argc, char** argv) {
   }
   std::free(pil);
   std::printf(
-      "{\"atan2\": [%lld, %lld, %lld], \"atan2_special\": %lld, \"sincos\": [%lld, %lld, %lld], \"sincos_worst\": [%lld, %lld, %lld], "
+      "{\"atan2\": [%lld, %lld, %lld], \"atan2_special\": %lld, \"atan2_rot\": [%lld, %lld, %lld], \"atan2_rot_special\": %lld, \"sincos\": [%lld, %lld, %lld], \"sincos_worst\": [%lld, %lld, %lld], "
       "\"atan2_max_rel_log2\": %.2f, \"pll_mismatch\": %lld, \"pll_chunks_rerun\": %lld, \"pll_steps\": %lld}\n",
-      at.n, at.certified, at.mismatch, at.special, sc.n, sc.certified, sc.mismatch, scw.n, scw.certified, scw.mismatch, std::log2(at.max_rel), pll_bad,
+      at.n, at.certified, at.mismatch, at.special, ar.n, ar.certified, ar.mismatch, ar.special, sc.n, sc.certified, sc.mismatch, scw.n, scw.certified, scw.mismatch, std::log2(at.max_rel), pll_bad,
       reruns, steps);
   return 0;
 }

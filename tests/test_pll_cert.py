@@ -29,11 +29,12 @@ def cert_bin(tmp_path_factory):
 def test_pll_fast_certificate(cert_bin, seed):
     r = json.loads(subprocess.run([cert_bin, "2000000", str(seed)], check=True, capture_output=True,
                                   text=True).stdout)
-    for k in ("atan2", "sincos", "sincos_worst"):
+    for k in ("atan2", "atan2_rot", "sincos", "sincos_worst"):
         n, certified, mismatch = r[k]
         assert mismatch == 0, (k, r)
         assert certified > 0.9 * n, (k, r)  # the fast path is the common path
     assert r["atan2_special"] == 0, r
+    assert r["atan2_rot_special"] == 0, r
     assert r["atan2_max_rel_log2"] < -45.5, r  # the fit's 2^-46.8 plus rounding, far inside the 2^-40 margin  # no subnormal / NaN errorD off x = y = 0 in the kernel's domain
     assert r["pll_mismatch"] == 0, r
     # re-run chunks are rare (8 steps each)
