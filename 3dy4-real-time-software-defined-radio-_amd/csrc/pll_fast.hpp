@@ -18,15 +18,19 @@
 //   - sincos: a three-term FMA Cody-Waite reduction of the fp32 argument
 //     (exact first step) instead of the double-double reduction; the sine and
 //     cosine kernels by Estrin's scheme; quadrant signs applied to the floats.
-// Each double result is within ~2^-46.5 (relative) of the exact value: the
-// atan polynomial's fit error plus a few ulps of rounding (tests/pll_cert.cpp).
+// Each double result is within ~2^-46.3 (relative) of the exact value: the
+// atan polynomial's fit error or the rotation's reciprocal plus a few ulps of
+// rounding (tests/pll_cert.cpp measures 2^-46.4 / 2^-46.7 / 2^-51.5 against
+// glibc for atan2_abs / atan2_rot / sincos).
 //
 // Certificate.  mid_score() measures a result's distance to the nearest float
 // midpoint; the caller keeps the running unsigned minimum over a chunk, which
 // is certified while it stays >= kCertified, i.e. every result lies more than
-// 4,095 double ulps (~2^-40 relative) from a midpoint -- so it, the exact
-// value and the library's result (within ~2^-46.5 and 1-2 ulps of the exact
-// value) round to one float.  The remaining cases are guarded by chunk_ok on the
+// kCertW = 1,024 double ulps (>= 2^-43 relative, 10x the error above) from a
+// midpoint -- so it, the exact value and the library's result (within
+// ~2^-46.3 and 1-2 ulps of the exact value) round to one float.  (The round-2
+// window of 4,096 ulps re-ran 4x as many chunks: 2.3 % of 64-lane chunks, a
+// 5 % slower recurrence.)  The remaining cases are guarded by chunk_ok on the
 // state before and after each chunk (finite and in range, so |trigArg| <
 // 2^26, trigArg != -0, the feedback floats are 0 or >= 2^-60, and errorD is
 // never subnormal; a NaN from x = y = 0 or a non-finite input reaches
@@ -70,11 +74,15 @@ constexpr double kP1 = 0x1.921fb54442d18p+0, kP2 = 0x1.1a62633145c07p-54;
 constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
 constexpr double kPi = 0x1.921fb54442d18p+1;
 
-// mid_score(d) = ((lo29 - (2^28 - 4096)) mod 2^29) << 3 for the 29 mantissa
-// bits double -> float drops: < kCertified <=> lo29 within [-4096, 4096) of
-// the midpoint 2^28.  One shift-add per result.
-constexpr unsigned kCertified = 8192u << 3;
-constexpr unsigned kMidBias = 0x80008000u;  // -((2^28 - 4096) << 3) mod 2^32
+// mid_score(d) = ((lo29 - (2^28 - W)) mod 2^29) << 3 for the 29 mantissa
+// bits double -> float drops: < kCertified <=> lo29 within [-W, W) of the
+// midpoint 2^28 (W = kCertW).  One shift-add per result.
+#ifndef SDR_PLL_CERT_W
+#define SDR_PLL_CERT_W 1024
+#endif
+constexpr unsigned kCertW = SDR_PLL_CERT_W;  // the window's half width in double ulps (a power of 2)
+constexpr unsigned kCertified = (2u * kCertW) << 3;
+constexpr unsigned kMidBias = 0u - (((1u << 28) - kCertW) << 3);  // -((2^28 - W) << 3) mod 2^32
 
 SDR_HD inline unsigned lo_bits(double d) { return (unsigned)__builtin_bit_cast(unsigned long long, d); }
 SDR_HD inline unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
@@ -212,7 +220,15 @@ SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score) 
 // certified (score 0, the chunk re-runs): a result that rounds to +-pi_f
 // (beta + delta may have crossed +-pi, where atan2 wraps).
 template <class Ops>
+SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned& score, double& res);
+template <class Ops>
 SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned& score) {
+  double res;
+  return atan2_rot<Ops>(y, x, v, o, score, res);
+}
+// res: the double result (the CPU test reads it to bound the error)
+template <class Ops>
+SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned& score, double& res) {
   const int q4 = o.q & 3;
   const double S = o.S, C = o.C;
   const double X = (double)x, Y = (double)y;
@@ -224,7 +240,7 @@ SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned&
   k = k == 3 ? -1 : k;
   k = (k == 2 && __builtin_signbit(o.r)) ? -2 : k;
   const double kd = (double)k;
-  const double res = Ops::fma(kd, kP1, -o.r) + Ops::fma(kd, kP2, d);
+  res = Ops::fma(kd, kP1, -o.r) + Ops::fma(kd, kP2, d);
   const float f = (float)res;
   const bool axis = y == 0.0f;
   // atan2(+-0, x) = +-0 for x > 0, +-pi (rounded: pi_f) for x < 0

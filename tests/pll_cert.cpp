@@ -74,11 +74,14 @@ static void check_atan2(float y, float x, Counts& c) {
 static void check_sincos(float x, Counts& c) {
   unsigned score = ~0u;
   float s, co;
-  sincos_fast<HostOps>(x, s, co, score);
+  Osc o;
+  sincos_fast<HostOps>(x, s, co, score, o);
   const float rs = (float)std::sin((double)x), rc = (float)std::cos((double)x);
   ++c.n;
   if (score < kCertified) return;
   ++c.certified;
+  track(c, o.S, std::sin((double)x));
+  track(c, o.C, std::cos((double)x));
   if (fbits(s) != fbits(rs) || fbits(co) != fbits(rc)) {
     if (c.mismatch < 5) std::fprintf(stderr, "sincos mismatch x=%a s=%a/%a c=%a/%a\n", x, s, rs, co, rc);
     ++c.mismatch;
@@ -96,13 +99,15 @@ static void check_atan2_rot(float arg, float v, Counts& c) {
   const float eI = (v == 0.0f ? 1.0f : v) * fbI;
   const float eQ = v * (-1.0f * fbQ);
   unsigned score = ~0u;
-  const float eD = atan2_rot<HostOps>(eQ, eI, v, o, score);
+  double res;
+  const float eD = atan2_rot<HostOps>(eQ, eI, v, o, score, res);
   const double refd = std::atan2((double)eQ, (double)eI);
   const float ref = (float)refd;
   ++c.n;
   if (float_special(eD)) ++c.special;
   if (score < kCertified) return;
   ++c.certified;
+  if (eQ != 0.0f) track(c, res, refd);
   if (fbits(eD) != fbits(ref)) {
     if (c.mismatch < 5)
       std::fprintf(stderr, "atan2_rot mismatch arg=%a v=%a fast=%a ref=%a\n", arg, v, (double)eD, (double)ref);
@@ -239,8 +244,9 @@ int main(int argc, char** argv) {
   std::free(pil);
   std::printf(
       "{\"atan2\": [%lld, %lld, %lld], \"atan2_special\": %lld, \"atan2_rot\": [%lld, %lld, %lld], \"atan2_rot_special\": %lld, \"sincos\": [%lld, %lld, %lld], \"sincos_worst\": [%lld, %lld, %lld], "
-      "\"atan2_max_rel_log2\": %.2f, \"pll_mismatch\": %lld, \"pll_chunks_rerun\": %lld, \"pll_steps\": %lld}\n",
-      at.n, at.certified, at.mismatch, at.special, ar.n, ar.certified, ar.mismatch, ar.special, sc.n, sc.certified, sc.mismatch, scw.n, scw.certified, scw.mismatch, std::log2(at.max_rel), pll_bad,
+      "\"atan2_max_rel_log2\": %.2f, \"atan2_rot_max_rel_log2\": %.2f, \"sincos_max_rel_log2\": %.2f, \"cert_window_ulps\": %u, \"pll_mismatch\": %lld, \"pll_chunks_rerun\": %lld, \"pll_steps\": %lld}\n",
+      at.n, at.certified, at.mismatch, at.special, ar.n, ar.certified, ar.mismatch, ar.special, sc.n, sc.certified, sc.mismatch, scw.n, scw.certified, scw.mismatch, std::log2(at.max_rel), std::log2(ar.max_rel),
+      std::log2(std::fmax(sc.max_rel, scw.max_rel)), kCertW, pll_bad,
       reruns, steps);
   return 0;
 }

@@ -35,7 +35,12 @@ def test_pll_fast_certificate(cert_bin, seed):
         assert certified > 0.9 * n, (k, r)  # the fast path is the common path
     assert r["atan2_special"] == 0, r
     assert r["atan2_rot_special"] == 0, r
-    assert r["atan2_max_rel_log2"] < -45.5, r  # the fit's 2^-46.8 plus rounding, far inside the 2^-40 margin  # no subnormal / NaN errorD off x = y = 0 in the kernel's domain
+    # the certificate's window (cert_window_ulps double ulps, >= 2^-43 relative)
+    # must exceed every fast result's error by a wide margin
+    assert r["cert_window_ulps"] <= 1024, r
+    assert r["atan2_rot_max_rel_log2"] < -45.5, r
+    assert r["sincos_max_rel_log2"] < -45.5, r
+    assert r["atan2_max_rel_log2"] < -45.5, r  # the fit's 2^-46.8 plus rounding
     assert r["pll_mismatch"] == 0, r
     # re-run chunks are rare (8 steps each)
     assert r["pll_chunks_rerun"] * 8 < 0.01 * r["pll_steps"], r
