@@ -16,8 +16,9 @@
 //     < 2^-46.8) by Estrin's scheme (depth 5) instead of OCML's degree 19 by
 //     Horner's (depth 20);
 //   - sincos: a three-term FMA Cody-Waite reduction of the fp32 argument
-//     (exact first step) instead of the double-double reduction; the sine and
-//     cosine kernels by Estrin's scheme; quadrant signs applied to the floats.
+//     (exact first step) instead of the double-double reduction; sine and
+//     cosine kernels one term shorter than fdlibm's, by Estrin's scheme;
+//     quadrant signs applied before the rounding to float.
 // Each double result is within ~2^-46.3 (relative) of the exact value: the
 // atan polynomial's fit error or the rotation's reciprocal plus a few ulps of
 // rounding (tests/pll_cert.cpp measures 2^-46.4 / 2^-46.7 / 2^-51.5 against
@@ -61,11 +62,15 @@ constexpr double kAtanC[16] = {
     -0x1.7459013f32a55p-4, 0x1.3af102625a079p-4, -0x1.1042b16ee39eep-4, 0x1.dae1c88757e5cp-5,
     -0x1.9852ad76ae65cp-5, 0x1.4cd7d6822d40bp-5, -0x1.e72bb0e3e1c37p-6, 0x1.2c694cfa120d0p-6,
     -0x1.231ab51098098p-7, 0x1.97372e16c0db6p-9, -0x1.68e74a9b5111ap-11, 0x1.2ddb1bd53fd3fp-14};
-// OCML's (fdlibm's) sine / cosine kernels on [-pi/4, pi/4]
-constexpr double kS1 = -0x1.5555555555555p-3, kS2 = 0x1.1111111110bb3p-7, kS3 = -0x1.a01a019e83e5cp-13,
-                 kS4 = 0x1.71de3796cde01p-19, kS5 = -0x1.ae600b42fdfa7p-26, kS6 = 0x1.5e0b2f9a43bb8p-33;
-constexpr double kC1 = 0x1.5555555555555p-5, kC2 = -0x1.6c16c16c16967p-10, kC3 = 0x1.a01a019f4ec90p-16,
-                 kC4 = -0x1.27e4fa17f65f6p-22, kC5 = 0x1.1eeb69037ab78p-29, kC6 = -0x1.907db46cc5e42p-37;
+// Sine / cosine kernels on [-pi/4, pi/4], one term shorter than OCML's
+// (fdlibm's, error 2^-58): weighted least-squares fits (scripts/fit_sincos.py)
+// with relative error < 2^-47.4 (sine) and 2^-53.1 (cosine), inside the
+// certificate's margin like the atan fit.
+//   sin r = r + r z (S1 + S2 z + ... + S5 z^4),  cos r = 1 - z/2 + z^2 (C1 + ... + C5 z^4)
+constexpr double kS1 = -0x1.55555555520b6p-3, kS2 = 0x1.1111110c7394ep-7, kS3 = -0x1.a019f92438b3ep-13,
+                 kS4 = 0x1.71d763ba62162p-19, kS5 = -0x1.a95eb720c4661p-26;
+constexpr double kC1 = 0x1.5555555552c07p-5, kC2 = -0x1.6c16c166fb086p-10, kC3 = 0x1.a019fa3cf03c1p-16,
+                 kC4 = -0x1.27dffdd9599aap-22, kC5 = 0x1.1bbaabead14f7p-29;
 // pi/2 = P1 + P2 (+ -1.5e-33); 2/pi; pi.  A third Cody-Waite term is not
 // needed: over every float in [pi/4, 2^26) the reduced argument is at least
 // 2^-27.83 (exhaustive search, at x = 0x1.f9cbe2p+7), so |kd| * 1.5e-33 <=
@@ -154,7 +159,7 @@ SDR_HD inline double atan2_abs(float y, float x, unsigned& score) {
 
 // The oscillator a fast step hands the next step's phase detector: the
 // reduced argument r (trigArg = r + q pi/2 + ~2^-84 |q|) and the double
-// sine S and cosine C of trigArg (the quadrant applied to fdlibm's kernels
+// sine S and cosine C of trigArg (the quadrant applied to the sine and cosine kernels
 // of r), from which atan2_rot rotates.
 struct Osc {
   double r, S, C;
@@ -174,12 +179,12 @@ SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score, 
   const int q = (int)kd;
   const double z = r * r;
   const double z2 = z * z;
-  // sin r = r + r^3 (S1 + z S'(z)), S' = (S2 + S3 z) + z^2 ((S4 + S5 z) + z^2 S6)
-  const double sp = Ops::fma(z2, Ops::fma(kS6, z2, Ops::fma(kS5, z, kS4)), Ops::fma(kS3, z, kS2));
-  const double sr = Ops::fma(r * z, Ops::fma(z, sp, kS1), r);
-  // cos r = (1 - z/2) + z^2 C(z), C = (C1 + C2 z) + z^2 ((C3 + C4 z) + z^2 (C5 + C6 z));
+  // sin r = r + r z S(z), S = (S1 + S2 z) + z^2 ((S3 + S4 z) + z^2 S5)  (Estrin)
+  const double sp = Ops::fma(z2, Ops::fma(kS5, z2, Ops::fma(kS4, z, kS3)), Ops::fma(kS2, z, kS1));
+  const double sr = Ops::fma(r * z, sp, r);
+  // cos r = (1 - z/2) + z^2 C(z), C = (C1 + C2 z) + z^2 ((C3 + C4 z) + z^2 C5);
   // 1 - z/2 in one rounding (cos r >= 0.7: 1 ulp, no compensation needed)
-  const double cp = Ops::fma(z2, Ops::fma(z2, Ops::fma(kC6, z, kC5), Ops::fma(kC4, z, kC3)), Ops::fma(kC2, z, kC1));
+  const double cp = Ops::fma(z2, Ops::fma(kC5, z2, Ops::fma(kC4, z, kC3)), Ops::fma(kC2, z, kC1));
   const double cr = Ops::fma(z2, cp, Ops::fma(z, -0.5, 1.0));
   score = umin(score, umin(mid_score(sr), mid_score(cr)));
   // quadrant q mod 4: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s), applied
