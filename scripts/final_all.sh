@@ -1,5 +1,5 @@
 set -u
-OUT=gpurun_out/final1; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-final1}; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1; tail -1 $OUT/smoke.log
 timeout -k 10 300 python bench.py > $OUT/bench_default.json 2>$OUT/bench.err || exit 1
