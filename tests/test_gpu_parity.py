@@ -551,6 +551,39 @@ def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
         assert_bits(res["1"][1][s], ost, f"stream {s} state vs oracle")
 
 
+def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch):
+    """The certified path (its rotation phase detector, the 1,024-ulp window
+    and the chunk guards) on inputs far from a pilot: magnitudes 2^-40..2^40
+    with random signs, 2 % exact zeros, constant and all-zero streams; every
+    result bitwise equal to the library path, 4 streams to the oracle."""
+    sdrhip = built_lib
+    rng = np.random.default_rng(11)
+    S, n, Fs = 256, 4096, 240e3
+    x = (rng.choice([-1.0, 1.0], (S, n)) * np.exp2(rng.uniform(-40, 40, (S, n)))).astype(np.float32)
+    x[rng.uniform(size=(S, n)) < 0.02] = 0.0
+    x[1] = 0.0
+    x[2] = 0.25
+    x[3] = -1e-3
+    st0 = np.tile(np.array([1, 0, 0, 0, 0, 1], np.float32), S)
+    A = sdrhip.DeviceArray
+    d_x = A.from_numpy(gpu_ctx, x)
+    res = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("SDR_PLL_FAST", fast)
+        d_pll = A.from_numpy(gpu_ctx, st0)
+        d_out = A(gpu_ctx, S * n * 4)
+        gpu_ctx.fm_pll_dev(d_x, n, S, n, 19e3, Fs, 2.0, 0.0, 0.01, d_pll, None, n, d_out, n)
+        gpu_ctx.synchronize()
+        res[fast] = (d_out.download().reshape(S, n), d_pll.download().reshape(S, 6))
+    assert_bits(res["1"][0], res["0"][0], "nco fast vs library")
+    assert_bits(res["1"][1], res["0"][1], "pll state fast vs library")
+    for s in (0, 1, 2, 3):
+        ost = st0[6 * s:6 * s + 6].copy()
+        nco = oracle.fm_pll(x[s], 19e3, Fs, 2.0, 0.0, 0.01, ost)
+        assert_bits(res["1"][0][s], nco, f"stream {s} vs oracle")
+        assert_bits(res["1"][1][s], ost, f"stream {s} state vs oracle")
+
+
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                                              (147, 1280, 101, 100, 12800), (3, 5, 101, 100, 5000)])
 def test_resample_plan_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, n):
