@@ -78,8 +78,8 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     static __device__ double rcp(double u) { return __builtin_amdgcn_rcp(u); }
   };
   unsigned score = 0u;
-  // the oscillator the previous fast step left: a chunk's steps 2..8 rotate
-  // back from it (pllfast::atan2_rot) instead of evaluating atan2
+  // the oscillator the previous step left: every step but the kernel's first
+  // rotates back from it (pllfast::atan2_rot) instead of evaluating atan2
   pllfast::Osc osc{0.0, 0.0, 1.0, 0};
   auto fast_step = [&](float v, auto rot) __attribute__((always_inline)) {
     const float eI = (v == 0.0f ? 1.0f : v) * fbI;
@@ -113,15 +113,18 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     // keep the loads here: left to the scheduler they sink to their use
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto run = [&](const float (&buf)[CH], long long k0) __attribute__((always_inline)) {
+  // first: the kernel's first chunk, whose step 1 has no oscillator to rotate
+  // from (the carried state holds only its floats) and runs the polynomial
+  auto run = [&](const float (&buf)[CH], long long k0, auto first) __attribute__((always_inline)) {
     if constexpr (FAST) {
       const float s0 = fbI, s1 = fbQ, s2 = integrator, s3 = phaseEst, s4 = trigOffset;
       score = start_ok ? ~0u : 0u;
       // unconditional: args rows hold n + 1 floats (launch_pll_recurrence), so
       // ar[n] is the row's spare slot -- no per-step bounds compare and branch
-      // step 1 on the polynomial (a rotating first step after fast chunks,
-      // behind a wave-uniform branch, measured 1 % slower)
-      fast_step(buf[0], poly_t{});
+      if constexpr (decltype(first)::value)
+        fast_step(buf[0], poly_t{});
+      else
+        fast_step(buf[0], rot_t{});
       ar[k0 + 1] = arg;
 #pragma unroll
       for (int j = 1; j < CH; ++j) {
@@ -142,17 +145,28 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
       pll_step(buf[j]);
       if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
     }
-    if constexpr (FAST) start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
+    if constexpr (FAST) {
+      start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
+      // the next chunk's first step rotates from the oscillator of this
+      // chunk's last argument (the library's floats are within an ulp of it)
+      float tq, ti;
+      unsigned unused = 0u;
+      pllfast::sincos_fast<DevOps>(arg, tq, ti, unused, osc);
+    }
   };
   // ping-pong register chunks (no copies, so no wait at the chunk boundary
   // beyond the chunk being consumed); a chunk past nc re-loads an in-bounds one
-  if (nc > 0) load(xa, 0);
-  for (long long k0 = 0; k0 < nc; k0 += 2 * CH) {
-    load(xb, k0 + CH < nc ? k0 + CH : k0);
-    run(xa, k0);
+  if (nc > 0) {
+    load(xa, 0);
+    load(xb, CH < nc ? CH : 0);
+    run(xa, 0, std::true_type{});
+  }
+  for (long long k0 = CH; k0 < nc; k0 += 2 * CH) {
+    load(xa, k0 + CH < nc ? k0 + CH : k0);
+    run(xb, k0, std::false_type{});
     if (k0 + CH < nc) {
-      load(xa, k0 + 2 * CH < nc ? k0 + 2 * CH : k0);
-      run(xb, k0 + CH);
+      load(xb, k0 + 2 * CH < nc ? k0 + 2 * CH : k0);
+      run(xa, k0 + CH, std::false_type{});
     }
   }
   for (long long k = nc; k < n; ++k) {  // ragged tail

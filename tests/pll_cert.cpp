@@ -130,7 +130,7 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
   r.trig = f.trig = trig0;
   long long bad_args = 0;
   bool start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig);
-  Osc osc{};  // the kernel's: a chunk's steps 2..8 rotate back from the previous step's oscillator
+  Osc osc{};  // the kernel's: every step but the first rotates back from the previous step's oscillator
   auto lib_step = [&](Pll& p, float v) {
     const float eI = (v == 0.0f ? 1.0f : v) * p.fbI;
     const float eQ = v * (-1.0f * p.fbQ);
@@ -153,7 +153,8 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
       const float v = in[k0 + j];
       const float eI = (v == 0.0f ? 1.0f : v) * f.fbI;
       const float eQ = v * (-1.0f * f.fbQ);
-      const float eD = j > 0 ? atan2_rot<HostOps>(eQ, eI, v, osc, score) : atan2_fast<HostOps>(eQ, eI, score);
+      const float eD =
+          (j > 0 || k0 > 0) ? atan2_rot<HostOps>(eQ, eI, v, osc, score) : atan2_fast<HostOps>(eQ, eI, score);
       f.integ = f.integ + Ki * eD;
       f.phase = f.phase + (Kp * eD + f.integ);
       f.trig = f.trig + 1.0f;
@@ -167,6 +168,9 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
       f = saved;
       for (long long j = 0; j < m; ++j) fa[j] = lib_step(f, in[k0 + j]);
       start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig);
+      float tq, ti;
+      unsigned unused = 0u;
+      sincos_fast<HostOps>(fa[m - 1], tq, ti, unused, osc);  // the kernel's refresh after a re-run
     }
     for (long long j = 0; j < m; ++j) bad_args += fbits(ra[j]) != fbits(fa[j]);
   }
