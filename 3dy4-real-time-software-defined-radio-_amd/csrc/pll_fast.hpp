@@ -219,7 +219,7 @@ SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score) 
 // (t^3/3 is < 2^-66 |beta|) and v_rcp_f64's 2^-24.4 costs < 2^-46 |beta|;
 // the numerator's one rounding costs 2^-53 |S C|.  So the result
 // beta + delta is within ~2^-45 |result| of the exact atan2 -- as tight as
-// the polynomial's -- in ~12 double operations instead of ~27.  y = 0 (v = 0,
+// the polynomial's -- in ~10 double operations instead of ~27.  y = 0 (v = 0,
 // where x = fbI is a different geometry, or fbQ = 0) takes atan2's exact
 // values on the axis, +-0 or +-pi (x != 0 here: fbI is never 0).  Not
 // certified (score 0, the chunk re-runs): a result that rounds to +-pi_f
@@ -239,13 +239,15 @@ SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned&
   const double X = (double)x, Y = (double)y;
   const double num = Ops::fma(Y, C, X * S);
   const double den = Ops::fma(X, C, -(Y * S));
-  const double d = num * Ops::rcp(den);
+  const double rc = Ops::rcp(den);
   // k = (2 [v < 0] - q4) mod 4 as a representative in (-pi, pi]
   int k = ((v < 0.0f ? 2 : 0) - q4) & 3;
   k = k == 3 ? -1 : k;
   k = (k == 2 && __builtin_signbit(o.r)) ? -2 : k;
   const double kd = (double)k;
-  res = Ops::fma(kd, kP1, -o.r) + Ops::fma(kd, kP2, d);
+  // beta + delta = k P1 + (delta - r): k P2 (<= 2^-52.5 of the result when k != 0,
+  // absent when k = 0) is dropped; two roundings of at most 2^-53 each
+  res = Ops::fma(kd, kP1, Ops::fma(num, rc, -o.r));
   const float f = (float)res;
   const bool axis = y == 0.0f;
   // atan2(+-0, x) = +-0 for x > 0, +-pi (rounded: pi_f) for x < 0
