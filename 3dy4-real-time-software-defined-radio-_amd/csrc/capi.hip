@@ -25,9 +25,16 @@ struct sdr_ctx {
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   int arith = SDR_ARITH_EXACT;
+  // sdr_stereo_pcm_u8_dev's launch order: -1 auto, 0 serial, 1 forked
+  // (sdr_ctx_set_stereo_fork; SDR_STEREO_FORK sets the default at creation)
+  int stereo_fork = -1;
   // grow-only device scratch for the host-pointer wrappers and internal use
   void* buf[19] = {};
   size_t cap[19] = {};
+  // live graphs recorded on this context: they hold pointers into buf[], so
+  // scratch() refuses to reallocate while any exists (or while capturing)
+  int graphs = 0;
+  bool grow_refused = false;
   std::string err;
 };
 
@@ -67,11 +74,27 @@ int enter(sdr_ctx* c) {
   return SDR_OK;
 }
 
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return s && hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+// Grow-only scratch.  A HIP graph recorded on the context keeps the buffer
+// pointers it was captured with, so growing (free + malloc) is refused --
+// nullptr, grow_refused set, see scratch_fail -- while any graph of the
+// context is alive or a capture is in progress: size the scratch with one
+// direct call of the largest shape first (bench.py and sdr_project do).
 void* scratch(sdr_ctx* c, int slot, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (c->cap[slot] >= bytes) return c->buf[slot];
+  if (c->graphs > 0 || capturing(c->cur) || capturing(c->side)) {
+    c->grow_refused = true;
+    return nullptr;
+  }
   if (c->buf[slot]) {
+    // the old buffer may still be in use on either stream
     (void)hipStreamSynchronize(c->cur);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     (void)hipFree(c->buf[slot]);
     c->buf[slot] = nullptr;
     c->cap[slot] = 0;
@@ -83,6 +106,19 @@ void* scratch(sdr_ctx* c, int slot, size_t bytes) {
   }
   c->cap[slot] = want;
   return c->buf[slot];
+}
+
+// The error for a scratch() that returned nullptr: a refused growth (a live
+// graph or a capture holds the old buffers) or an allocation failure.
+int scratch_fail(sdr_ctx* c, const char* what) {
+  if (c->grow_refused) {
+    c->grow_refused = false;
+    return fail(c, SDR_EINVAL,
+                "%s: scratch would have to grow while a graph recorded on this context is alive or being captured "
+                "(run one direct call of the largest shape before capturing, or destroy the graphs first)",
+                what);
+  }
+  return fail(c, SDR_ENOMEM, "%s", what);
 }
 
 // Shared validation of the stateful FIR family (src/filter.cpp:66-83, 123-140).
@@ -179,6 +215,8 @@ int sdr_ctx_create(int device, sdr_ctx** out) {
     return SDR_EHIP;
   }
   c->cur = c->own;
+  c->stereo_fork = sdr::env_int("SDR_STEREO_FORK", -1);
+  if (c->stereo_fork > 1 || c->stereo_fork < -1) c->stereo_fork = -1;
   *out = c;
   return SDR_OK;
 }
@@ -187,9 +225,9 @@ int sdr_ctx_destroy(sdr_ctx* c) {
   if (!c) return SDR_EINVAL;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->cur);
+  if (c->side) (void)hipStreamSynchronize(c->side);
   for (void* b : c->buf)
     if (b) (void)hipFree(b);
-  if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->own) (void)hipStreamDestroy(c->own);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->fork) (void)hipEventDestroy(c->fork);
@@ -210,6 +248,13 @@ int sdr_ctx_set_arith(sdr_ctx* c, int mode) {
   if (!c) return SDR_EINVAL;
   if (mode != SDR_ARITH_EXACT && mode != SDR_ARITH_FMA) return fail(c, SDR_EINVAL, "unknown arithmetic mode %d", mode);
   c->arith = mode;
+  return SDR_OK;
+}
+
+int sdr_ctx_set_stereo_fork(sdr_ctx* c, int mode) {
+  if (!c) return SDR_EINVAL;
+  if (mode < -1 || mode > 1) return fail(c, SDR_EINVAL, "unknown stereo fork mode %d", mode);
+  c->stereo_fork = mode;
   return SDR_OK;
 }
 
@@ -348,6 +393,7 @@ int sdr_event_destroy(sdr_ctx* c, sdr_event* ev) {
 struct sdr_graph {
   hipGraph_t g = nullptr;
   hipGraphExec_t exec = nullptr;
+  sdr_ctx* owner = nullptr;  // whose scratch the recorded launches point into
 };
 
 int sdr_graph_begin(sdr_ctx* c) {
@@ -371,6 +417,8 @@ int sdr_graph_end(sdr_ctx* c, sdr_graph** out) {
     delete g;
     return hip_fail(c, h, "stream capture");
   }
+  g->owner = c;
+  ++c->graphs;
   *out = g;
   return SDR_OK;
 }
@@ -389,6 +437,7 @@ int sdr_graph_destroy(sdr_ctx* c, sdr_graph* g) {
   if (g) {
     if (g->exec) (void)hipGraphExecDestroy(g->exec);
     if (g->g) (void)hipGraphDestroy(g->g);
+    if (g->owner && g->owner->graphs > 0) --g->owner->graphs;
     delete g;
   }
   return SDR_OK;
@@ -522,7 +571,7 @@ static int frontend_dev(sdr_ctx* c, sdr::Src src, int D, const float* I, const f
     const size_t bytes = (size_t)nout * (size_t)nstreams * sizeof(float);
     y0 = static_cast<float*>(scratch(c, kY0, bytes));
     y1 = static_cast<float*>(scratch(c, kY1, bytes));
-    if (!y0 || !y1) return fail(c, SDR_ENOMEM, "scratch for decimated I/Q (%zu B)", bytes);
+    if (!y0 || !y1) return scratch_fail(c, "scratch for decimated I/Q");
   }
   hipError_t e = sdr::launch_fir(a, h, true, 2, src, c->cur, y0, y1, fast);
   if (e != hipSuccess) return hip_fail(c, e, "frontend launch");
@@ -574,7 +623,7 @@ static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long 
     return sdr_fir_decim_f32_dev(c, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride);
   }
   float* hp = static_cast<float*>(scratch(c, kTmp, sdr::resample_scratch_floats(up, ntaps) * sizeof(float)));
-  if (!hp) return fail(c, SDR_ENOMEM, "polyphase table");
+  if (!hp) return scratch_fail(c, "polyphase table");
   hipError_t e = sdr::launch_resample(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, hp,
                                       c->cur, lp_tables);
   if (e != hipSuccess) return hip_fail(c, e, "resample launch");
@@ -612,6 +661,12 @@ int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int n
       (void)hipFree(p->tables);
       delete p;
       return hip_fail(c, e, "resample plan tables");
+    } else if ((e = hipStreamSynchronize(c->cur)) != hipSuccess) {
+      // built before the plan is handed out: a later call may run on
+      // another stream (sdr_ctx_set_stream), which nothing would order
+      (void)hipFree(p->tables);
+      delete p;
+      return hip_fail(c, e, "resample plan tables");
     }
   }
   *out = p;
@@ -623,7 +678,8 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
   if (rc) return rc;
   if (p) {
     if (p->tables) {
-      (void)hipStreamSynchronize(c->cur);
+      // every stream that used the plan, not only the current one
+      (void)hipDeviceSynchronize();
       (void)hipFree(p->tables);
     }
     delete p;
@@ -649,7 +705,7 @@ int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, 
   if ((reinterpret_cast<uintptr_t>(x) & 15) || (nstreams > 1 && x_stride % 8))
     return fail(c, SDR_EINVAL, "fp16 input rows must be 16-B aligned (x_stride %% 8 == 0)");
   uint32_t* pairs = static_cast<uint32_t*>(scratch(c, kTmp, sdr::fir_long_h_pairs(ntaps) * sizeof(uint32_t)));
-  if (!pairs) return fail(c, SDR_ENOMEM, "tap pair table");
+  if (!pairs) return scratch_fail(c, "tap pair table");
   hipError_t e = sdr::launch_fir_long_h(x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, pairs, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "fir_block_f16 launch");
   return SDR_OK;
@@ -708,7 +764,7 @@ int sdr_mono_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
   float* demod = static_cast<float*>(scratch(c, kPipe0, (size_t)nstreams * dstride * sizeof(float)));
   float* delayed = static_cast<float*>(scratch(c, kPipe1, (size_t)nstreams * dstride * sizeof(float)));
   float* audio = static_cast<float*>(scratch(c, kPipe2, (size_t)nstreams * astride * sizeof(float)));
-  if (!demod || !delayed || !audio) return fail(c, SDR_ENOMEM, "pipeline buffers");
+  if (!demod || !delayed || !audio) return scratch_fail(c, "pipeline buffers");
   if ((rc = sdr_frontend_u8_dev(c, D, iq, npairs, nstreams, iq_stride, h_rf, rf_taps, state_i, state_q, ns_rf, prev_i,
                                 prev_q, demod, dstride)))
     return rc;
@@ -730,7 +786,7 @@ int sdr_fm_pll_dev(sdr_ctx* c, const float* in, long long n, int nstreams, long 
     return fail(c, SDR_EINVAL, "stream strides overlap");
   const long long astride = (n + 1 + 3) / 4 * 4;  // trigArg per sample (+ the incoming nco_state)
   float* args = static_cast<float*>(scratch(c, kPipe6, (size_t)nstreams * astride * sizeof(float)));
-  if (!args) return fail(c, SDR_ENOMEM, "pll argument buffer");
+  if (!args) return scratch_fail(c, "pll argument buffer");
   hipError_t e = sdr::launch_pll(in, n, nstreams, in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix,
                                  mix_stride, out, out_stride, args, astride, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "pll launch");
@@ -773,7 +829,7 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
   float* args = static_cast<float*>(scratch(c, kPipe6, (size_t)nstreams * pstride * sizeof(float)));
   float* mixed = static_cast<float*>(scratch(c, kPipe7, dbytes));
   if (!demod || !delayed || !mono || !pilot || !sband || !slp || !args || !mixed)
-    return fail(c, SDR_ENOMEM, "pipeline buffers");
+    return scratch_fail(c, "pipeline buffers");
   if (!c->side) {
     SDR_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     SDR_HIP(c, hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
@@ -793,10 +849,10 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
   // wave) leaves most of the chip idle: at 1,024 streams (16 waves) the side
   // branch runs in the gaps (stereo0 -1.6 %), at 16,384 (256 waves, one per
   // CU) it competes with the latency-bound recurrence for the CUs and slows
-  // it (stereo0w +14 %, same box).  SDR_STEREO_FORK=0/1 forces either way.
-  static const int fork_env = sdr::env_int("SDR_STEREO_FORK", -1);
+  // it (stereo0w +14 %, same box).  sdr_ctx_set_stereo_fork (default from
+  // SDR_STEREO_FORK at context creation) forces either way.
   const long long pll_waves = (nstreams + 63) / 64;
-  const bool fork = fork_env >= 0 ? fork_env != 0 : 4 * pll_waves <= sdr::device_cu_count();
+  const bool fork = c->stereo_fork >= 0 ? c->stereo_fork != 0 : 4 * pll_waves <= sdr::device_cu_count();
   if (fork) {
     SDR_HIP(c, hipEventRecord(c->fork, c->cur));
     SDR_HIP(c, hipStreamWaitEvent(c->side, c->fork, 0));
@@ -812,9 +868,15 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
     if (!rc)
       rc = sdr_fir_block_f32_dev(c, demod, nd, nstreams, dstride, taps->h_stereo, taps->bpf_taps, st->stereo_state,
                                  st->ns_bpf, sband, dstride);
-    hipError_t e = (rc || !fork) ? hipSuccess : hipEventRecord(c->join, c->side);
+    // the join is recorded even when a side-branch call failed, and then
+    // waited on here, so nothing left on the side stream overlaps later
+    // main-stream work or a scratch free
+    hipError_t e = fork ? hipEventRecord(c->join, c->side) : hipSuccess;
     c->cur = main;
-    if (rc) return rc;
+    if (rc) {
+      if (fork && e == hipSuccess) (void)hipStreamWaitEvent(main, c->join, 0);
+      return rc;
+    }
     if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   }
   // :120: pilot band-pass, then the PLL recurrence (:123-126: 19 kHz, ncoScale 2,
@@ -874,7 +936,7 @@ int sdr_fir_decim_f32(sdr_ctx* c, int D, const float* x, long long n, const floa
   float* dh = static_cast<float*>(scratch(c, kH, ntaps * sizeof(float)));
   float* ds = static_cast<float*>(scratch(c, kS0, (ns ? ns : 1) * sizeof(float)));
   float* dy = static_cast<float*>(scratch(c, kY0, nout * sizeof(float)));
-  if (!dx || !dh || !ds || !dy) return fail(c, SDR_ENOMEM, "scratch");
+  if (!dx || !dh || !ds || !dy) return scratch_fail(c, "scratch");
   SDR_HIP(c, hipMemcpyAsync(dx, x, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
   SDR_HIP(c, hipMemcpyAsync(dh, h, ntaps * sizeof(float), hipMemcpyHostToDevice, c->cur));
   if (ns) SDR_HIP(c, hipMemcpyAsync(ds, state, ns * sizeof(float), hipMemcpyHostToDevice, c->cur));
@@ -902,7 +964,7 @@ int sdr_resample_f32(sdr_ctx* c, int up, int down, const float* x, long long n, 
   float* dh = static_cast<float*>(scratch(c, kH, ntaps * sizeof(float)));
   float* ds = static_cast<float*>(scratch(c, kS0, (ns ? ns : 1) * sizeof(float)));
   float* dy = static_cast<float*>(scratch(c, kY0, (ny ? ny : 1) * sizeof(float)));
-  if (!dx || !dh || !ds || !dy) return fail(c, SDR_ENOMEM, "scratch");
+  if (!dx || !dh || !ds || !dy) return scratch_fail(c, "scratch");
   if (n > 0) SDR_HIP(c, hipMemcpyAsync(dx, x, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
   if (ntaps > 0) SDR_HIP(c, hipMemcpyAsync(dh, h, ntaps * sizeof(float), hipMemcpyHostToDevice, c->cur));
   if (ns) SDR_HIP(c, hipMemcpyAsync(ds, state, ns * sizeof(float), hipMemcpyHostToDevice, c->cur));
@@ -923,7 +985,7 @@ int sdr_fm_demod_f32(sdr_ctx* c, const float* I, const float* Q, long long n, fl
   float* dq = static_cast<float*>(scratch(c, kX1, n * sizeof(float)));
   float* dp = static_cast<float*>(scratch(c, kPrev, 4 * sizeof(float)));
   float* dout = static_cast<float*>(scratch(c, kOut, n * sizeof(float)));
-  if (!di || !dq || !dp || !dout) return fail(c, SDR_ENOMEM, "scratch");
+  if (!di || !dq || !dp || !dout) return scratch_fail(c, "scratch");
   SDR_HIP(c, hipMemcpyAsync(di, I, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
   SDR_HIP(c, hipMemcpyAsync(dq, Q, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
   SDR_HIP(c, hipMemcpyAsync(dp, prev_i, sizeof(float), hipMemcpyHostToDevice, c->cur));
@@ -952,17 +1014,17 @@ static int frontend_host(sdr_ctx* c, sdr::Src src, int D, const float* I, const 
   if (src == sdr::Src::F32) {
     dx0 = static_cast<float*>(scratch(c, kX0, n * sizeof(float)));
     dx1 = static_cast<float*>(scratch(c, kX1, n * sizeof(float)));
-    if (!dx0 || !dx1) return fail(c, SDR_ENOMEM, "scratch");
+    if (!dx0 || !dx1) return scratch_fail(c, "scratch");
   } else {
     du = static_cast<uint8_t*>(scratch(c, kX0, 2 * n));
-    if (!du) return fail(c, SDR_ENOMEM, "scratch");
+    if (!du) return scratch_fail(c, "scratch");
   }
   float* dh = static_cast<float*>(scratch(c, kH, ntaps * sizeof(float)));
   float* ds0 = static_cast<float*>(scratch(c, kS0, (ns ? ns : 1) * sizeof(float)));
   float* ds1 = static_cast<float*>(scratch(c, kS1, (ns ? ns : 1) * sizeof(float)));
   float* dp = static_cast<float*>(scratch(c, kPrev, 4 * sizeof(float)));
   float* dout = static_cast<float*>(scratch(c, kOut, nout * sizeof(float)));
-  if (!dh || !ds0 || !ds1 || !dp || !dout) return fail(c, SDR_ENOMEM, "scratch");
+  if (!dh || !ds0 || !ds1 || !dp || !dout) return scratch_fail(c, "scratch");
   if (src == sdr::Src::F32) {
     SDR_HIP(c, hipMemcpyAsync(dx0, I, n * sizeof(float), hipMemcpyHostToDevice, c->cur));
     SDR_HIP(c, hipMemcpyAsync(dx1, Q, n * sizeof(float), hipMemcpyHostToDevice, c->cur));

@@ -58,18 +58,24 @@
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
+// SDR_IQ_PF: LDS chunk reads in flight ahead of the scan in fir_tile_iq
+#ifndef SDR_IQ_PF
+#define SDR_IQ_PF 3
+#endif
 
 namespace sdr {
 namespace {
-__device__ __forceinline__ float4 ldg_stream(const float4* p) {
+typedef float nf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ nf4 ldg_stream_n(const float4* p) {
 #if SDR_FIR_NT
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
+  return __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
 #else
-  return *p;
+  return *reinterpret_cast<const nf4*>(p);
 #endif
 }
+// a staged chunk as HIP's float4 (fir_tile) or the native vector (fir_tile_iq)
+__device__ __forceinline__ void set_chunk(float4& d, const nf4& v) { d = make_float4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ void set_chunk(nf4& d, const nf4& v) { d = v; }
 __device__ __forceinline__ uint2 ldg_stream(const uint2* p) {
 #if SDR_FIR_NT_U8
   typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -81,6 +87,18 @@ __device__ __forceinline__ uint2 ldg_stream(const uint2* p) {
 }
 }  // namespace
 }  // namespace sdr
+
+#ifdef SDR_FIR_TRACE
+// Diagnostic builds only (scripts/build_ab_tree.sh trace -DSDR_FIR_TRACE):
+// per-workgroup timeline of fir_tile's first tile, read back by
+// tools/fir_trace.py through sdr_debug_fir_trace().  Never in the product
+// library.  Per workgroup, 8 words: HW_ID | XCC_ID << 32, s_memrealtime at
+// entry, then s_memtime sums over the workgroup's tiles of: the wait for a
+// tile's loads (top of the tile -> landed), staging, scan, epilogue; the
+// tile count; s_memrealtime at the end.
+constexpr int kTraceWG = 1 << 17;
+__device__ unsigned long long g_fir_trace[kTraceWG * 8];
+#endif
 
 namespace sdr {
 namespace {
@@ -199,20 +217,20 @@ __device__ __forceinline__ bool interior(const TileRef& tr, long long n) {
 // u8 coalesced vectors).  Chunk addresses are clamped into the block, so an
 // edge tile loads in-bounds but partly wrong data that edge_fill() then
 // overwrites.  No wait: stage_store consumes the registers.
-template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC, bool CLAMP>
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC, bool CLAMP, class V>
 __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, int tid,
-                                           float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
-                                           float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+                                           V (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                           V (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   using G = Geom<D, T, R, DEMOD, NW>;
-  auto load4 = [&](int i, float4& a0, float4& a1) {
+  auto load4 = [&](int i, V& a0, V& a1) {
     long long p = tr.pb + 4LL * i;
     if constexpr (CLAMP) {
       const long long pmax = (n & ~3LL) - 4;  // last whole aligned chunk
       p = p < 0 ? 0 : (p > pmax ? pmax : p);
     }
     if constexpr (SRC == Src::F32) {
-      a0 = ldg_stream(reinterpret_cast<const float4*>(tr.x0 + p));
-      if (NCH == 2) a1 = ldg_stream(reinterpret_cast<const float4*>(tr.x1 + p));
+      set_chunk(a0, ldg_stream_n(reinterpret_cast<const float4*>(tr.x0 + p)));
+      if (NCH == 2) set_chunk(a1, ldg_stream_n(reinterpret_cast<const float4*>(tr.x1 + p)));
     } else {
       const uint2 b = ldg_stream(reinterpret_cast<const uint2*>(tr.iq + 2 * p));
       // the raw wire bytes stay in the prefetch registers (2 VGPRs per
@@ -231,10 +249,10 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
 }
 
 // Clamped loads only where the span leaves the block (workgroup-uniform).
-template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC, class V>
 __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int tid,
-                                           float4 (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
-                                           float4 (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
+                                           V (&v0)[Geom<D, T, R, DEMOD, NW>::FULL + 1],
+                                           V (&v1)[Geom<D, T, R, DEMOD, NW>::FULL + 1]) {
   if (tr.pb >= 0 && tr.pb + Geom<D, T, R, DEMOD, NW>::LDS_LEN <= n)
     stage_load_impl<D, T, R, DEMOD, NW, NCH, SRC, false>(tr, n, tid, v0, v1);
   else
@@ -245,13 +263,12 @@ __device__ __forceinline__ void stage_load(const TileRef& tr, long long n, int t
 // straddles n when n % 4 != 0): after the clamped vector fill, rewrite the
 // span elements a stored output reads whose chunk was clamped -- the old
 // state before the block, [pb, 0), and the true samples of the straddling
-// chunk, [n & ~3, n).  With `strip`, also stage the block's last STRIP
-// inputs (old state where p < 0) for tile 0's state carry.  The loads are
-// issued in batches of four per thread before any LDS write, so an edge tile
-// costs about one memory latency, not one per element.
-template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC>
-__device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long n, int ns, float* lds0, float* lds1,
-                                          bool strip, float* strip0, float* strip1, int c0 = 0) {
+// chunk, [n & ~3, n).  put(i, v0, v1) stores span element i of the two
+// channels in the kernel's LDS layout.  The loads are issued in batches of
+// four per thread before any LDS write, so an edge tile costs about one
+// memory latency, not one per element.
+template <int D, int T, int R, bool DEMOD, int NW, int NCH, Src SRC, class Put>
+__device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long n, int ns, Put&& put, int c0 = 0) {
   using G = Geom<D, T, R, DEMOD, NW>;
   const long long n4 = n & ~3LL;
   const int lo_end = tr.pb < 0 ? (int)(-tr.pb < G::LDS_LEN ? -tr.pb : G::LDS_LEN) : 0;
@@ -259,44 +276,24 @@ __device__ __forceinline__ void edge_fill(const TileRef& tr, int tid, long long 
   const int hi_beg = clampi(n4 - tr.pb, lo_end, G::LDS_LEN);
   const int hi_end = clampi(n - tr.pb, hi_beg, G::LDS_LEN);
   const int nfix = lo_end + (hi_end - hi_beg);
-  const int ntot = nfix + (strip ? G::STRIP : 0);
-  for (int e0 = 0; e0 < ntot; e0 += 4 * G::NTH) {
+  for (int e0 = 0; e0 < nfix; e0 += 4 * G::NTH) {
     float v0[4], v1[4];
-    float* d0[4];
-    float* d1[4];
+    int idx[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = e0 + u * G::NTH + tid;
-      long long p;
-      if (e < lo_end) {
-        p = tr.pb + e;
-        d0[u] = lds0 + e;
-        d1[u] = lds1 + e;
-      } else if (e < nfix) {
-        const int i = hi_beg + (e - lo_end);
-        p = tr.pb + i;
-        d0[u] = lds0 + i;
-        d1[u] = lds1 + i;
-      } else {
-        const int j = e - nfix;
-        p = n - G::STRIP + j;
-        d0[u] = strip0 + j;
-        d1[u] = strip1 + j;
-      }
+      idx[u] = e < lo_end ? e : hi_beg + (e - lo_end);
+      const long long p = tr.pb + idx[u];
       v0[u] = 0.0f;
       v1[u] = 0.0f;
-      if (e < ntot) {
+      if (e < nfix) {
         v0[u] = edge_at<SRC>(tr.x0, tr.iq, c0, tr.st0, ns, n, p);
         if (NCH == 2) v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (e0 + u * G::NTH + tid < ntot) {
-        *d0[u] = v0[u];
-        if (NCH == 2) *d1[u] = v1[u];
-      }
-    }
+    for (int u = 0; u < 4; ++u)
+      if (e0 + u * G::NTH + tid < nfix) put(idx[u], v0[u], v1[u]);
   }
   // Retire the edge loads inside the (rare) edge path.  Left pending, they
   // make hipcc's waitcnt pass merge the edge and interior paths
@@ -384,6 +381,17 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     last = min((x + 1) * per_xcd, total);
   }
   if (first >= last) return;
+#ifdef SDR_FIR_TRACE
+  unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime();
+#define SDR_TRACE_AT(i)                                        \
+  {                                                            \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    if ((i) > 0) tr_sum[(i) - 1] += now_ - tr_last;            \
+    tr_last = now_;                                            \
+  }
+#else
+#define SDR_TRACE_AT(i)
+#endif
 
   using Stage = float4[G::FULL + 1];
   Stage sa0, sa1;
@@ -415,13 +423,22 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     // stages the block's last STRIP inputs (old state where p < 0: the
     // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
     // rewrites the state below.
+    SDR_TRACE_AT(0);
     __syncthreads();
+#ifdef SDR_FIR_TRACE
+    __builtin_amdgcn_s_waitcnt(0);
+    SDR_TRACE_AT(1);
+#endif
     stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
     if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       __syncthreads();
-      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, lds0, lds1, false, strip0, strip1);
+      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, [&](int i, float v0, float v1) {
+        lds0[i] = v0;
+        if (NCH == 2) lds1[i] = v1;
+      });
     }
     __syncthreads();
+    SDR_TRACE_AT(2);
     if (lin + step < last && a.ablate != 1)
       stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + step), n, tid, v0, v1);
 
@@ -505,6 +522,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       }
     }
 
+    SDR_TRACE_AT(3);
     const long long m0 = tr.m_start + (long long)wave * G::WADV + (long long)R * lane;  // this lane's first output
     if constexpr (DEMOD) {
       // ---- 3. discriminator in registers.  The decimated sample before
@@ -634,6 +652,298 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     }
   };
 
+#ifdef SDR_FIR_TRACE
+  for (int lin = first; lin < last; lin += step) {
+    tile(lin, sa0, sa1);
+    SDR_TRACE_AT(4);
+    ++tr_n;
+  }
+  if (tid == 0 && blockIdx.x < kTraceWG) {
+    unsigned long long* o = g_fir_trace + 8ull * blockIdx.x;
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    o[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    o[1] = tr_r0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[2 + i] = tr_sum[i];
+    o[6] = tr_n;
+    o[7] = __builtin_amdgcn_s_memrealtime();
+  }
+#else
+  for (int lin = first; lin < last; lin += step) tile(lin, sa0, sa1);
+#endif
+}
+#undef SDR_TRACE_AT
+
+// ------------------------------------------------- I/Q-paired fused kernel --
+// fir_tile_iq: the fused front end (2 channels + discriminator) with I and Q
+// of each span position side by side in LDS, so one packed instruction
+// carries both channels: per tap and output
+//   v_pk_mul_f32 p, s[h_k pair] (op_sel broadcast of h_k), {I, Q}
+//   v_pk_add_f32 {accI, accQ}, {accI, accQ}, p
+// Each half is an IEEE single multiply and add rounded separately, exactly
+// the reference's two operations (src/filter.cpp:129-137): same bits as
+// fir_tile, half the FIR instructions, and the tap operand rides in the
+// SGPR pair the scalar loads already fill (no extra SGPRs).
+//
+// Layout: span position p holds {I, Q} at float index at(p) = 2p + 4*(p /
+// PADP).  PADP = D*R is the lane-window stride, so every lane's window
+// starts on a pad boundary and its chunk offsets are compile-time
+// constants; the 16-B pad makes the lane stride 44 dwords instead of 40,
+// which puts the 16 lanes of each ds_read_b128 group on 16 distinct 4-bank
+// slots (40 dwords give only 8: a 2-way conflict on every read).
+template <int D, int T, int R>
+struct IQGeom {
+  using G = Geom<D, T, R, true, 1>;
+  static constexpr int PADP = D * R;
+  static_assert(PADP % 4 == 0, "a staged 4-position chunk never straddles a pad");
+  static constexpr int LEN = 2 * G::LDS_LEN + 4 * ((G::LDS_LEN + PADP - 1) / PADP);
+  static constexpr int SMEM = LEN > 2 * G::STRIP ? LEN : 2 * G::STRIP;  // floats
+  static constexpr int LANE = 2 * PADP + 4;  // floats between adjacent lane windows
+  __device__ static __forceinline__ int at(int p) { return 2 * p + 4 * (p / PADP); }
+};
+
+// Tiles [first, last) by `step` this workgroup walks (see fir_tile).
+__device__ __forceinline__ void tile_walk(const FirLaunch& a, int total, int& first, int& step, int& last) {
+  if (a.walk == 0) {
+    first = blockIdx.x * a.tiles_per_wg;
+    step = 1;
+    last = min(first + a.tiles_per_wg, total);
+  } else {
+    const int per_xcd = (total + 7) / 8;
+    const int x = blockIdx.x & 7;
+    step = gridDim.x >> 3;
+    first = x * per_xcd + (blockIdx.x >> 3);
+    last = min((x + 1) * per_xcd, total);
+  }
+}
+
+template <int D, int T, int R, Src SRC, bool FMA = false>
+__global__ __launch_bounds__(64) void fir_tile_iq(FirLaunch a, const float* __restrict__ h) {
+  using G = Geom<D, T, R, true, 1>;
+  using P = IQGeom<D, T, R>;
+  constexpr int NW = 1, NCH = 2;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* strip0 = smem;  // tile 0, after its scan: the block's last inputs, planar
+  float* strip1 = smem + G::STRIP;
+
+  const int tid = threadIdx.x;
+  const int lane = tid;
+  const long long n = a.n;
+  const long long nout = n / D;
+  const int ns = a.ns;
+  int first, step, last;
+  tile_walk(a, a.nstreams * a.tiles_per_stream, first, step, last);
+  if (first >= last) return;
+
+  using Stage = f4[G::FULL + 1];
+  Stage sa0, sa1;
+#pragma unroll
+  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = f4{0.f, 0.f, 0.f, 0.f};
+  if (a.ablate != 1)
+    stage_load<D, T, R, true, NW, NCH, SRC>(tile_ref<D, T, R, true, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
+
+  auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
+    const TileRef tr = tile_ref<D, T, R, true, NW, NCH, SRC>(a, lin);
+    float old_pi = 0.0f, old_pq = 0.0f;
+    if (tr.t == 0) {  // workgroup-uniform; scalar loads (see fir_tile)
+      using cf = const __attribute__((address_space(4))) float*;
+      const int s = __builtin_amdgcn_readfirstlane(tr.s);
+      old_pi = ((cf)a.prev0)[s];
+      old_pq = ((cf)a.prev1)[s];
+    }
+
+    // ---- 1. registers -> LDS, I/Q interleaved; prefetch the next tile
+    __syncthreads();
+    {
+      auto put = [&](int i, const f4& a0, const f4& a1) {
+        float* d = smem + P::at(4 * i);
+        if constexpr (SRC == Src::U8) {
+          // 8 wire bytes = I0 Q0 I1 Q1 | I2 Q2 I3 Q3: already the pair order
+          const uint32_t bx = __float_as_uint(a0.x), by = __float_as_uint(a0.y);
+          *reinterpret_cast<f4*>(d) = f4{u8_byte_to_f32<0>(bx), u8_byte_to_f32<1>(bx), u8_byte_to_f32<2>(bx),
+                                         u8_byte_to_f32<3>(bx)};
+          *reinterpret_cast<f4*>(d + 4) = f4{u8_byte_to_f32<0>(by), u8_byte_to_f32<1>(by), u8_byte_to_f32<2>(by),
+                                             u8_byte_to_f32<3>(by)};
+        } else {
+          // whole-vector shuffles of native vectors (element access of HIP
+          // float4s here pushed the stage arrays to scratch)
+          *reinterpret_cast<f4*>(d) = __builtin_shufflevector(a0, a1, 0, 4, 1, 5);
+          *reinterpret_cast<f4*>(d + 4) = __builtin_shufflevector(a0, a1, 2, 6, 3, 7);
+        }
+      };
+#pragma unroll
+      for (int it = 0; it < G::FULL; ++it) put(tid + it * G::NTH, v0[it], v1[it]);
+      if (G::REM && tid < G::REM) put(tid + G::FULL * G::NTH, v0[G::FULL], v1[G::FULL]);
+    }
+    if (tr.t == 0 || !interior<D, T, R, true, NW>(tr, n)) {  // workgroup-uniform
+      __syncthreads();
+      edge_fill<D, T, R, true, NW, NCH, SRC>(tr, tid, n, ns, [&](int i, float e0, float e1) {
+        *reinterpret_cast<f2*>(smem + P::at(i)) = f2{e0, e1};
+      });
+    }
+    __syncthreads();
+    if (lin + step < last && a.ablate != 1)
+      stage_load<D, T, R, true, NW, NCH, SRC>(tile_ref<D, T, R, true, NW, NCH, SRC>(a, lin + step), n, tid, v0, v1);
+
+    // ---- 2. the lane's window: chunk c = positions 2c, 2c+1 = {I, Q, I, Q}
+    f2 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = f2{0.0f, 0.0f};
+    const float* w = smem + P::LANE * lane;
+    if (a.ablate == 2) {
+      acc[0] = *reinterpret_cast<const f2*>(w);
+    } else {
+      // taps as SGPR pairs {h_k, h_k+1}, NPASS passes over consecutive tap
+      // ranges (every output still visits k = 0..T-1 in order)
+      constexpr int NPASS = SDR_NPASS, KP = ((T + NPASS - 1) / NPASS + 1) / 2 * 2;
+      using hconst = const __attribute__((address_space(4))) float*;
+      const hconst hc = (hconst)h;
+      f2 hp[KP / 2];
+      static_for<0, NPASS>([&](auto pi) {
+        constexpr int k0 = decltype(pi)::value * KP;
+        constexpr int k1 = k0 + KP < T ? k0 + KP : T;
+        if constexpr (k0 < T) {
+          if (a.ablate == 4 && k0 > 0) return;
+#pragma unroll
+          for (int i = 0; i < (k1 - k0 + 1) / 2; ++i)
+            hp[i] = f2{hc[k0 + 2 * i], k0 + 2 * i + 1 < k1 ? hc[k0 + 2 * i + 1] : 0.0f};
+#pragma unroll
+          for (int i = 0; i < (k1 - k0 + 1) / 2; ++i) asm volatile("" : "+s"(hp[i]));
+          constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
+          constexpr int whi = G::HALO + D * (R - 1) - k0;
+          constexpr int clo = wlo / 2, chi = whi / 2;
+          auto chunk = [&](int c) { return *reinterpret_cast<const f4*>(w + 4 * c + 4 * ((2 * c) / P::PADP)); };
+          // LDS reads PF chunks ahead: a chunk is only ~8 packed
+          // instructions of work, far shorter than an LDS read's latency
+          constexpr int PF = SDR_IQ_PF, NB = PF + 1;
+          f4 buf[NB];
+          static_for<0, PF>([&](auto pi2) {
+            constexpr int c = chi - decltype(pi2)::value;
+            if constexpr (c >= clo) buf[c % NB] = chunk(c);
+          });
+          static_for<0, chi - clo + 1>([&](auto ci) {
+            constexpr int c = chi - decltype(ci)::value;
+            if constexpr (c - PF >= clo) buf[(c - PF) % NB] = chunk(c - PF);
+            const f4 q = buf[c % NB];
+            const f2 e[2] = {f2{q.x, q.y}, f2{q.z, q.w}};
+            static_for<0, 2>([&](auto ji) {
+              constexpr int j = 1 - decltype(ji)::value;
+              static_for<0, R>([&](auto ri) {
+                constexpr int r = decltype(ri)::value;
+                constexpr int k = G::HALO + D * r - (2 * c + j);
+                if constexpr (k >= k0 && k < k1) {
+                  const float hk = ((k - k0) & 1) ? hp[(k - k0) / 2].y : hp[(k - k0) / 2].x;
+                  if constexpr (FMA)
+                    acc[r] = __builtin_elementwise_fma(f2{hk, hk}, e[j], acc[r]);
+                  else
+                    acc[r] = acc[r] + f2{hk, hk} * e[j];
+                }
+              });
+            });
+#pragma unroll
+            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+            __builtin_amdgcn_sched_barrier(0);
+          });
+        }
+      });
+    }
+
+    // ---- 3. discriminator in registers (as fir_tile)
+    const long long m0 = tr.m_start + (long long)R * lane;
+    {
+      float pI = __shfl_up(acc[R - 1].x, 1, 64);
+      float pQ = __shfl_up(acc[R - 1].y, 1, 64);
+      const bool first_out = tr.t == 0 && tid == 0;
+      if (first_out) {
+        pI = old_pi;
+        pQ = old_pq;
+      }
+      float d[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float ip = r ? acc[r - 1].x : pI;
+        const float qp = r ? acc[r - 1].y : pQ;
+        d[r] = demod_one(acc[r].x, acc[r].y, ip, qp);
+      }
+      float* o = a.out + (long long)tr.s * a.out_stride;
+      const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+      if ((lane >= 1 || first_out) && (a.ablate != 3 || d[0] == 12345.0f)) {
+        if (vec && m0 + R <= nout) {
+          if constexpr (R == 2) {
+            if constexpr (SDR_OUT_NT && SRC == Src::F32)
+              __builtin_nontemporal_store(f2{d[0], d[1]}, reinterpret_cast<f2*>(o + m0));
+            else
+              *reinterpret_cast<f2*>(o + m0) = f2{d[0], d[1]};
+          } else if constexpr (R == 4) {
+            *reinterpret_cast<f4*>(o + m0) = f4{d[0], d[1], d[2], d[3]};
+          } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (m0 + r < nout) o[m0 + r] = d[r];
+        }
+      }
+    }
+
+    // ---- 4. state carry (tile 0 only), planar strips as in fir_tile
+    if (tr.t == 0) {
+      __syncthreads();
+      for (int j0 = 0; j0 < G::STRIP; j0 += 4 * G::NTH) {
+        float s0[4], s1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * G::NTH + tid;
+          const long long p = n - G::STRIP + j;
+          s0[u] = s1[u] = 0.0f;
+          if (j < G::STRIP) {
+            s0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+            s1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * G::NTH + tid;
+          if (j < G::STRIP) {
+            strip0[j] = s0[u];
+            strip1[j] = s1[u];
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      // prev_* <- last decimated I/Q (src/filter.cpp:100-101), reference order
+      if (tid < 2) {
+        using hconst = const __attribute__((address_space(4))) float*;
+        const hconst hc = (hconst)h;
+        const float* sp = (tid == 0 ? strip0 : strip1) + (G::STRIP - D);
+        float y = 0.0f;
+#pragma unroll 8
+        for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
+        (tid == 0 ? a.prev0 : a.prev1)[tr.s] = y;
+      }
+      // state <- last ns input samples (src/filter.cpp:139)
+      if (ns <= G::STRIP) {
+        for (int j = tid; j < ns; j += G::NTH) {
+          tr.st0[j] = strip0[G::STRIP - ns + j];
+          tr.st1[j] = strip1[G::STRIP - ns + j];
+        }
+      } else {
+        for (int j = tid; j < ns; j += G::NTH) {
+          const long long p = n - ns + j;
+          tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, p);
+          tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
+        }
+      }
+    }
+  };
+
   for (int lin = first; lin < last; lin += step) tile(lin, sa0, sa1);
 }
 
@@ -710,7 +1020,7 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 // ------------------------------------------------------------ dispatch ----
 // Persistent grid: about `wpc` waves per CU (or the tile count, if smaller),
 // each workgroup walking its share of the tiles (see `walk` in fir_tile).
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false, bool IQ = false>
 hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
@@ -739,9 +1049,15 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
   }
   static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
   a.ablate = ablate;
-  const size_t lds = (size_t)G::SMEM * sizeof(float);
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st,
-                     a, h);
+  if constexpr (IQ) {
+    static_assert(NW == 1 && NCH == 2 && DEMOD, "the I/Q-paired kernel is the fused one-wave front end");
+    const size_t lds = (size_t)IQGeom<D, T, R>::SMEM * sizeof(float);
+    hipLaunchKernelGGL((fir_tile_iq<D, T, R, SRC, FMA>), dim3((unsigned)blocks), dim3(64), lds, st, a, h);
+  } else {
+    const size_t lds = (size_t)G::SMEM * sizeof(float);
+    hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds,
+                       st, a, h);
+  }
   return hipGetLastError();
 }
 
@@ -783,11 +1099,20 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
     if constexpr (DEMOD) {
       // SDR_ARITH_FMA: instantiated for the fused kernels; any other shape
       // runs the exact arithmetic (inside the tolerance)
+      // SDR_FIR_IQ=1 (A/B only): the I/Q-paired packed kernel instead of
+      // the planar one (same bits; 8 % slower on cfg2)
+      static const bool iq = env_int("SDR_FIR_IQ", 0) != 0;
       switch (a.D) {
         case 10:
+          if (iq)
+            return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true, true>(a, h, st, v.wpc)
+                         : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, false, true>(a, h, st, v.wpc);
           return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, v.wpc)
                        : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         case 5:
+          if (iq)
+            return a.fma ? run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, true, true>(a, h, st, v.wpc)
+                         : run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, false, true>(a, h, st, v.wpc);
           return a.fma ? run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, v.wpc)
                        : run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
         default: break;
@@ -867,3 +1192,15 @@ hipError_t launch_fir(const FirLaunch& a, const float* h, bool demod, int nch, S
 }
 
 }  // namespace sdr
+
+#ifdef SDR_FIR_TRACE
+extern "C" int sdr_debug_fir_trace(void* dst, size_t bytes, int reset) {
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fir_trace)) != hipSuccess) return -2;
+    return hipMemset(p, 0, sizeof g_fir_trace) == hipSuccess ? 0 : -2;
+  }
+  if (bytes > sizeof g_fir_trace) bytes = sizeof g_fir_trace;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fir_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif

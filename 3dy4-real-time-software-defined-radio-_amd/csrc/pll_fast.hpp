@@ -15,8 +15,9 @@
 //     the IEEE division sequence; a degree-15 polynomial in t^2 (error
 //     < 2^-46.8) by Estrin's scheme (depth 5) instead of OCML's degree 19 by
 //     Horner's (depth 20);
-//   - sincos: a three-term FMA Cody-Waite reduction of the fp32 argument
-//     (exact first step) instead of the double-double reduction; sine and
+//   - sincos: a two-term FMA Cody-Waite reduction of the fp32 argument
+//     (exact first step; a third term changes no result, see kP1 below)
+//     instead of the double-double reduction; sine and
 //     cosine kernels one term shorter than fdlibm's, by Estrin's scheme;
 //     quadrant signs applied before the rounding to float.
 // Each double result is within ~2^-46.3 (relative) of the exact value: the
@@ -34,8 +35,9 @@
 // 5 % slower recurrence.)  The remaining cases are guarded by chunk_ok on the
 // state before and after each chunk (finite and in range, so |trigArg| <
 // 2^26, trigArg != -0, the feedback floats are 0 or >= 2^-60, and errorD is
-// never subnormal; a NaN from x = y = 0 or a non-finite input reaches
-// phaseEst and fails the closing check).  Within those guards a certified
+// never subnormal), and by input_ok on the chunk's samples (0 or 2^-60 <=
+// |v| <= FLT_MAX, so the phase detector's products are normal or exact
+// zeros); a NaN from x = y = 0 reaches phaseEst and fails the closing check.  Within those guards a certified
 // step's floats are the reference's; an uncertified chunk is re-run with the
 // library routines.  DESIGN.md section 4.7 has the argument.
 //
@@ -101,6 +103,19 @@ SDR_HD inline bool chunk_ok(float fbI, float fbQ, float integrator, float phaseE
   return (int)(trigOffset >= 0.0f) & (int)(trigOffset < 0x1p24f) & (int)(__builtin_fabsf(phaseEst) < 0x1p24f) &
          (int)(__builtin_fabsf(integrator) < 0x1p20f) & (int)(aI <= 1.0f) & (int)(aQ <= 1.0f) &
          ((int)(aI >= 0x1p-60f) | (int)(fbI == 0.0f)) & ((int)(aQ >= 0x1p-60f) | (int)(fbQ == 0.0f));
+}
+
+// Chunk guard on the inputs: every sample v of a certified chunk is 0 or
+// 2^-60 <= |v| <= FLT_MAX.  With chunk_ok's feedback floats (0 or >= 2^-60)
+// the phase detector's products v * fbI and v * fbQ are then normal floats
+// (>= 2^-120, each within 2^-24 of the exact product) or exact zeros, which
+// atan2_rot's error bound assumes; a tiny or subnormal v can round a product
+// to a subnormal or to 0 (v = 2^-149 once gave a residual of 3e-3 rad), and
+// a non-finite v has no product at all.  A chunk with any other input is
+// re-run with the library routines.
+SDR_HD inline bool input_ok(float v) {
+  const float a = __builtin_fabsf(v);
+  return (int)(v == 0.0f) | ((int)(a >= 0x1p-60f) & (int)(a <= 0x1.fffffep127f));
 }
 
 // A float that is NaN, Inf or subnormal.  In chunk_ok's domain errorD is

@@ -118,7 +118,11 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   auto run = [&](const float (&buf)[CH], long long k0, auto first) __attribute__((always_inline)) {
     if constexpr (FAST) {
       const float s0 = fbI, s1 = fbQ, s2 = integrator, s3 = phaseEst, s4 = trigOffset;
-      score = start_ok ? ~0u : 0u;
+      // the chunk's inputs (already in registers, off the recurrence's chain)
+      int in_ok = 1;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) in_ok &= (int)pllfast::input_ok(buf[j]);
+      score = (start_ok && in_ok) ? ~0u : 0u;
       // unconditional: args rows hold n + 1 floats (launch_pll_recurrence), so
       // ar[n] is the row's spare slot -- no per-step bounds compare and branch
       if constexpr (decltype(first)::value)

@@ -34,6 +34,7 @@ HEADER_PATH = os.path.join(REPO_DIR, "include", "sdr_hip.h")
 
 SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_ENODEV = 0, -1, -2, -3, -4
 ARITH_EXACT, ARITH_FMA = 0, 1  # sdr_ctx_set_arith modes
+FORK_AUTO, FORK_SERIAL, FORK_SIDE = -1, 0, 1  # sdr_ctx_set_stereo_fork modes
 
 _lib = None
 
@@ -53,6 +54,7 @@ _SIGS = {
     "sdr_ctx_get_stream": [_vp],
     "sdr_ctx_synchronize": [_vp],
     "sdr_ctx_set_arith": [_vp, _i],
+    "sdr_ctx_set_stereo_fork": [_vp, _i],
     "sdr_ctx_last_error": [_vp],
     "sdr_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "sdr_dev_free": [_vp, _vp],
@@ -205,9 +207,15 @@ class Graph:
         self._ctx._check(lib().sdr_graph_launch(self._ctx._c, self._g), "graph_launch")
 
     def close(self):
-        if self._g:
+        if self._g and self._ctx._c:
             lib().sdr_graph_destroy(self._ctx._c, self._g)
-            self._g = _vp()
+        self._g = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class ResamplePlan:
@@ -258,6 +266,11 @@ class Context:
         """FIR arithmetic of the fused front end: ARITH_EXACT (the reference's
         bits, default) or ARITH_FMA (one fused multiply-add per tap)."""
         self._check(lib().sdr_ctx_set_arith(self._c, mode), "set_arith")
+
+    def set_stereo_fork(self, mode: int):
+        """stereo_pcm_u8_dev's launch order: FORK_AUTO (side branch on a
+        second stream at <= CUs/4 PLL waves), FORK_SERIAL or FORK_SIDE."""
+        self._check(lib().sdr_ctx_set_stereo_fork(self._c, mode), "set_stereo_fork")
 
     def set_stream(self, hip_stream: int | None):
         """Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""

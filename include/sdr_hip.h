@@ -78,6 +78,17 @@ const char *sdr_ctx_last_error(sdr_ctx *ctx);
 #define SDR_ARITH_FMA 1
 int sdr_ctx_set_arith(sdr_ctx *ctx, int mode);
 
+/* Launch order of sdr_stereo_pcm_u8_dev (same outputs either way):
+ * SDR_FORK_SIDE runs the branches that do not wait for the PLL recurrence on
+ * a second HIP stream beside it, SDR_FORK_SERIAL runs everything on the
+ * context's stream, SDR_FORK_AUTO (default) forks while the recurrence
+ * occupies at most CUs/4 waves (<= 4,096 streams on MI355X).  The default
+ * at creation can be set by the environment variable SDR_STEREO_FORK. */
+#define SDR_FORK_AUTO (-1)
+#define SDR_FORK_SERIAL 0
+#define SDR_FORK_SIDE 1
+int sdr_ctx_set_stereo_fork(sdr_ctx *ctx, int mode);
+
 /* Device memory helpers so a C/C++ caller needs no HIP headers. */
 int sdr_dev_alloc(sdr_ctx *ctx, size_t bytes, void **ptr);
 int sdr_dev_free(sdr_ctx *ctx, void *ptr);
@@ -105,7 +116,12 @@ int sdr_event_destroy(sdr_ctx *ctx, sdr_event *ev);
  * carry across replays exactly as across direct calls).  Replaces the
  * per-block launch sequence of a streaming caller (src/project.cpp:289-318
  * runs one block at a time) by one launch.  The stream must not be the null
- * stream; calls that synchronise fail while capturing. */
+ * stream; calls that synchronise fail while capturing.
+ * A graph replays the context's internal scratch buffers it was recorded
+ * with, so while any graph of the context is alive (or a capture is in
+ * progress) a call that would need larger scratch fails with SDR_EINVAL
+ * instead of reallocating under the graph: make one direct call of the
+ * largest shape before capturing, or destroy the graphs first. */
 typedef struct sdr_graph sdr_graph;
 int sdr_graph_begin(sdr_ctx *ctx);
 int sdr_graph_end(sdr_ctx *ctx, sdr_graph **graph);

@@ -82,7 +82,7 @@ def harness(built_lib, tmp_path_factory):
     out = tmp_path_factory.mktemp("harness") / "dropin_harness"
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
                     os.path.join(REPO, "tests", "dropin_harness.cpp"), "-o", str(out),
-                    "-L", PKG, "-ldy4filter_hip", "-lsdrhip", f"-Wl,-rpath,{PKG}"], check=True)
+                    "-L", PKG, "-ldy4filter_hip", "-lsdrhip", f"-Wl,-rpath,{PKG}", "-pthread"], check=True)
     return str(out)
 
 

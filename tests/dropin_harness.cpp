@@ -12,11 +12,13 @@
 //   resample   U M x h ns block nblk y states
 //   demod      I Q prev_i prev_q out prevs  a0 b0 a1 b1 ...   (segments)
 //   frontend   D iq_u8 h block nblk out states
+//   threads    D iq_a iq_b h h_bpf block nblk out_a out_b   (two threads at once)
 //   glue       x pilot outdir
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sdr_filter_api.h"
@@ -132,6 +134,43 @@ int main(int argc, char** argv) {
     }
     save(argv[7], out);
     save(argv[8], sts);
+  } else if (op == "threads") {
+    // Two host threads inside the drop-in at once, each with its own stream
+    // and state vectors (src/project.cpp:299-302 calls it from two threads
+    // per block; here both run their whole block loops concurrently):
+    // per block, the front end (as "frontend" above) and blockConvolveFIR of
+    // the demodulated block -- out: demod ++ band-passed, block after block.
+    const int D = std::atoi(argv[2]);
+    const auto iqa = load<unsigned char>(argv[3]);
+    const auto iqb = load<unsigned char>(argv[4]);
+    const auto h = load<float>(argv[5]);
+    const auto hb = load<float>(argv[6]);
+    const long block = std::atol(argv[7]);
+    const int nblk = std::atoi(argv[8]);
+    auto work = [&](const std::vector<unsigned char>& iq, std::vector<float>& out) {
+      std::vector<float> si(100, 0.0f), sq(100, 0.0f), sb(100, 0.0f), yi, yq, dm, bp;
+      float pi = 0, pq = 0;
+      for (int b = 0; b < nblk; b++) {
+        std::vector<float> xi(block), xq(block);
+        for (long k = 0; k < block; k++) {
+          xi[k] = float(((unsigned char)iq[2 * (b * block + k)] - 128) / 128.0);
+          xq[k] = float(((unsigned char)iq[2 * (b * block + k) + 1] - 128) / 128.0);
+        }
+        downsampleBlockConvolveFIR(D, yi, xi, h, si);
+        downsampleBlockConvolveFIR(D, yq, xq, h, sq);
+        fmDemodArctan(yi, yq, pi, pq, dm);
+        blockConvolveFIR(bp, dm, hb, sb);
+        append(out, dm);
+        append(out, bp);
+      }
+    };
+    std::vector<float> outa, outb;
+    std::thread ta(work, std::cref(iqa), std::ref(outa));
+    std::thread tb(work, std::cref(iqb), std::ref(outb));
+    ta.join();
+    tb.join();
+    save(argv[9], outa);
+    save(argv[10], outb);
   } else if (op == "glue") {
     // the host-side rows, in the order tests/golden/make_golden.py ran them
     const auto x = load<float>(argv[2]);

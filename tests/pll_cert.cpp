@@ -148,7 +148,9 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
     float ra[8], fa[8];
     for (long long j = 0; j < m; ++j) ra[j] = lib_step(r, in[k0 + j]);
     const Pll saved = f;
-    unsigned score = start_ok ? ~0u : 0u;
+    bool in_ok = true;
+    for (long long j = 0; j < m; ++j) in_ok = in_ok && input_ok(in[k0 + j]);
+    unsigned score = start_ok && in_ok ? ~0u : 0u;
     for (long long j = 0; j < m; ++j) {
       const float v = in[k0 + j];
       const float eI = (v == 0.0f ? 1.0f : v) * f.fbI;
@@ -245,7 +247,22 @@ int main(int argc, char** argv) {
     pll_bad += pll_compare(pil, L, trig0, &reruns);
     steps += L;
   }
+  // tiny, subnormal and non-finite pilot samples (input_ok's excluded range,
+  // 2^-149 .. 2^-60, +-0, Inf, NaN): such chunks must re-run, never certify
+  long long tiny_bad = 0, tiny_reruns = 0;
+  for (int s = 0; s < 12; ++s) {
+    for (long long k = 0; k < L; ++k) {
+      const double amp = 0.2 * std::cos(2 * M_PI * 19e3 / 240e3 * (double)k + s);
+      pil[k] = (float)amp;
+      if (k % 61 == s) pil[k] = (float)logu(-149.0, -60.0);  // tiny and subnormal
+      if (k % 499 == 7) pil[k] = (k & 1) ? -0.0f : 0.0f;
+    }
+    if (s == 10) pil[L / 2] = INFINITY;
+    if (s == 11) pil[L / 3] = NAN;
+    tiny_bad += pll_compare(pil, L, s % 2 ? 0.0f : 1.6e7f, &tiny_reruns);
+  }
   std::free(pil);
+  std::printf("{\"pll_tiny_mismatch\": %lld, \"pll_tiny_reruns\": %lld}\n", tiny_bad, tiny_reruns);
   std::printf(
       "{\"atan2\": [%lld, %lld, %lld], \"atan2_special\": %lld, \"atan2_rot\": [%lld, %lld, %lld], \"atan2_rot_special\": %lld, \"sincos\": [%lld, %lld, %lld], \"sincos_worst\": [%lld, %lld, %lld], "
       "\"atan2_max_rel_log2\": %.2f, \"atan2_rot_max_rel_log2\": %.2f, \"sincos_max_rel_log2\": %.2f, \"cert_window_ulps\": %u, \"pll_mismatch\": %lld, \"pll_chunks_rerun\": %lld, \"pll_steps\": %lld}\n",

@@ -554,13 +554,18 @@ def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
 def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch):
     """The certified path (its rotation phase detector, the 1,024-ulp window
     and the chunk guards) on inputs far from a pilot: magnitudes 2^-40..2^40
-    with random signs, 2 % exact zeros, constant and all-zero streams; every
+    with random signs, 2 % exact zeros, 1 % tiny or subnormal samples
+    (2^-149..2^-60), constant and all-zero streams; every
     result bitwise equal to the library path, 4 streams to the oracle."""
     sdrhip = built_lib
     rng = np.random.default_rng(11)
     S, n, Fs = 256, 4096, 240e3
     x = (rng.choice([-1.0, 1.0], (S, n)) * np.exp2(rng.uniform(-40, 40, (S, n)))).astype(np.float32)
     x[rng.uniform(size=(S, n)) < 0.02] = 0.0
+    # tiny and subnormal samples (2^-149 .. 2^-60): outside pllfast::input_ok,
+    # their chunks must re-run on the library path
+    tiny = rng.uniform(size=(S, n)) < 0.01
+    x[tiny] = (rng.choice([-1.0, 1.0], tiny.sum()) * np.exp2(rng.uniform(-149, -60, tiny.sum()))).astype(np.float32)
     x[1] = 0.0
     x[2] = 0.25
     x[3] = -1e-3

@@ -1,0 +1,248 @@
+"""Bench-scale parity of the device pipelines, and the library under
+concurrent host threads.
+
+* The mono and stereo programs (sdr_mono_pcm_u8_dev / sdr_stereo_pcm_u8_dev,
+  src/project.cpp:72-133 + 304-314) at the stream counts bench.py runs them
+  (mono0 / stereo0: 1,024 streams; stereo0w: 16,384 -- here 4,160, already
+  past the 4,096 streams where the stereo call stops forking its side
+  branch), two consecutive blocks, every stream's PCM bytes and every carried
+  state word (the PLL's six floats included) against the oracle chain, which
+  tests/test_dropin.py pins to the reference program's own output.  Both
+  launch orders of the stereo call are run: forked (side branch on a second
+  HIP stream) and serial, chosen automatically and forced per context.
+* Two host threads, each with its own context on the same GPU, running the
+  bench's launch pattern (direct calls and a captured HIP graph replayed)
+  at the same time; and two threads inside the filter.h drop-in at once
+  (src/project.cpp:299-302 calls it from two threads per block).  Every
+  output bitwise against the oracle.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import assert_bits
+from test_dropin import _mono_setup, _stereo_setup, _stereo_state0
+
+pytestmark = pytest.mark.gpu
+
+WORKERS = 16  # the GPU box's CPU share (os.cpu_count() there reports the whole machine)
+
+
+def _pmap(fn, items):
+    """The oracle is C behind ctypes (the GIL is released inside each call)."""
+    with cf.ThreadPoolExecutor(WORKERS) as ex:
+        return list(ex.map(fn, items))
+
+
+def _synth_blocks(gpu_ctx, sdrhip, nstreams, npairs, nblk, seed):
+    """nblk device-synthesised u8 IQ blocks [nstreams][2*npairs], also on the host."""
+    A = sdrhip.DeviceArray
+    out = []
+    for b in range(nblk):
+        d = A(gpu_ctx, nstreams * 2 * npairs)
+        gpu_ctx.synth_fm_u8_dev(d, npairs, nstreams, 2 * npairs, seed=seed + 1000 * b)
+        gpu_ctx.synchronize()
+        out.append((d, d.download(np.uint8).reshape(nstreams, 2 * npairs)))
+    return out
+
+
+@pytest.mark.parametrize("nstreams,fork", [(1024, "auto"), (1024, "serial"), (4160, "auto"), (4160, "side")])
+def test_stereo_pipeline_bench_scale(gpu_ctx, oracle, built_lib, nstreams, fork):
+    """stereo0's shape (mode 0, 51,200-pair blocks): 1,024 streams fork the
+    side branch by default, 4,160 run serially by default; each is also
+    forced the other way.  Two blocks; all PCM and all state bitwise."""
+    sdrhip = built_lib
+    mode = 0
+    rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
+    npairs = block_bytes // 2
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    blocks = _synth_blocks(gpu_ctx, sdrhip, nstreams, npairs, 2, 4242 + nstreams)
+    A = sdrhip.DeviceArray
+    d_taps = {k: A.from_numpy(gpu_ctx, v) for k, v in taps.items()}
+    t = sdrhip.StereoTaps(d_taps["rf"].ptr, 101, d_taps["audio"].ptr, len(taps["audio"]), d_taps["pilot"].ptr,
+                          d_taps["stereo"].ptr, 101)
+    st0 = _stereo_state0()
+    d_st = {k: A.from_numpy(gpu_ctx, np.tile(v, nstreams)) for k, v in st0.items() if k != "prev"}
+    d_pi = A.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    d_pq = A.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    state = sdrhip.StereoState(d_st["i"].ptr, d_st["q"].ptr, 100, d_pi.ptr, d_pq.ptr, d_st["delay"].ptr, 50,
+                               d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr, d_st["stereo"].ptr,
+                               100, d_st["pll"].ptr)
+    pcm_stride = 2 * na + 2
+    d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
+    mode_id = {"auto": sdrhip.FORK_AUTO, "serial": sdrhip.FORK_SERIAL, "side": sdrhip.FORK_SIDE}[fork]
+    ost = [_stereo_state0() for _ in range(nstreams)]
+    gpu_ctx.set_stereo_fork(mode_id)
+    try:
+        for b, (d_iq, h_iq) in enumerate(blocks):
+            gpu_ctx.stereo_pcm_u8_dev(D, d_iq, npairs, nstreams, 2 * npairs, up, down, audio_fs, t, state, d_pcm,
+                                      pcm_stride)
+            gpu_ctx.synchronize()
+            got = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :2 * na]
+            want = _pmap(lambda s: oracle.stereo(D, h_iq[s], taps["rf"], ost[s], up, down, taps["audio"],
+                                                 taps["pilot"], taps["stereo"], audio_fs), range(nstreams))
+            bad = [s for s in range(nstreams) if not np.array_equal(got[s], want[s])]
+            assert not bad, f"{fork}: PCM of {len(bad)} streams differs in block {b} (first {bad[:8]})"
+            for k in ("pll", "pilot", "stereo", "stereo_lp", "audio", "delay", "i", "q"):
+                assert_bits(d_st[k].download().reshape(nstreams, -1), np.stack([o[k] for o in ost]),
+                            f"{fork} {k} block {b}")
+            prev = np.stack([d_pi.download(), d_pq.download()], axis=1)
+            assert_bits(prev, np.stack([o["prev"] for o in ost]), f"{fork} prev block {b}")
+    finally:
+        gpu_ctx.set_stereo_fork(sdrhip.FORK_AUTO)
+
+
+def test_mono_pipeline_bench_scale(gpu_ctx, oracle, built_lib):
+    """mono0's shape: 1,024 streams x 51,200-pair mode-0 blocks, two blocks;
+    every stream's PCM and carried state bitwise against the oracle chain."""
+    sdrhip = built_lib
+    mode, nstreams = 0, 1024
+    rf_fs, D, up, down, block_bytes, h_rf, h_audio = _mono_setup(oracle, mode)
+    npairs = block_bytes // 2
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    blocks = _synth_blocks(gpu_ctx, sdrhip, nstreams, npairs, 2, 777)
+    A = sdrhip.DeviceArray
+    d_hrf, d_ha = A.from_numpy(gpu_ctx, h_rf), A.from_numpy(gpu_ctx, h_audio)
+    z = lambda k: A.from_numpy(gpu_ctx, np.zeros(nstreams * k, np.float32))  # noqa: E731
+    si, sq, pi, pq, sd, sa = z(100), z(100), z(1), z(1), z(50), z(100)
+    pcm_stride = na + 4
+    d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
+    ost = [dict(i=np.zeros(100, np.float32), q=np.zeros(100, np.float32), prev=np.zeros(2, np.float32),
+                delay=np.zeros(50, np.float32), audio=np.zeros(100, np.float32)) for _ in range(nstreams)]
+    for b, (d_iq, h_iq) in enumerate(blocks):
+        gpu_ctx.mono_pcm_u8_dev(D, d_iq, npairs, nstreams, 2 * npairs, d_hrf, len(h_rf), si, sq, 100, pi, pq, sd, 50,
+                                up, down, d_ha, len(h_audio), sa, 100, d_pcm, pcm_stride)
+        gpu_ctx.synchronize()
+        got = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :na]
+        want = _pmap(lambda s: oracle.mono(D, h_iq[s], h_rf, ost[s]["i"], ost[s]["q"], ost[s]["prev"],
+                                           ost[s]["delay"], up, down, h_audio, ost[s]["audio"]), range(nstreams))
+        bad = [s for s in range(nstreams) if not np.array_equal(got[s], want[s])]
+        assert not bad, f"PCM of {len(bad)} streams differs in block {b} (first {bad[:8]})"
+        for k, d in (("i", si), ("q", sq), ("delay", sd), ("audio", sa)):
+            assert_bits(d.download().reshape(nstreams, -1), np.stack([o[k] for o in ost]), f"{k} block {b}")
+        prev = np.stack([pi.download(), pq.download()], axis=1)
+        assert_bits(prev, np.stack([o["prev"] for o in ost]), f"prev block {b}")
+
+
+def test_two_host_threads_two_contexts(built_lib, oracle):
+    """bench.py --gpus N's pattern, twice on one GPU at once: each host thread
+    owns a Context(0) (its own HIP stream and scratch) and runs the cfg2 front
+    end -- a direct call, two calls captured into a HIP graph and replayed,
+    another direct call -- three rounds, all concurrently with the other
+    thread.  Outputs and carried state bitwise against the oracle."""
+    sdrhip = built_lib
+    from sdrhip.synth import fm_planar
+
+    D, n, nstreams, nblk, rounds = 10, 65540, 24, 4, 3
+    nout = n // D
+    h = oracle.taps_lpf(2.4e6, 100e3, 101, 1)
+    inputs, wants = [], []
+    for th in range(2):
+        I = np.empty((nblk, nstreams, n), np.float32)
+        Q = np.empty_like(I)
+        for s in range(nstreams):
+            i, q = fm_planar(n * nblk, seed=500 + 97 * th + s)
+            I[:, s], Q[:, s] = i.reshape(nblk, n), q.reshape(nblk, n)
+        inputs.append((I, Q))
+        want = np.empty((nblk, nstreams, nout), np.float32)
+        states = []
+        for s in range(nstreams):
+            si, sq, pv = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
+            for b in range(nblk):
+                want[b, s] = oracle.frontend(D, I[b, s], Q[b, s], h, si, sq, pv)
+            states.append((si, sq, pv))
+        wants.append((want, states))
+    errors = []
+    barrier = threading.Barrier(2)
+
+    def worker(th):
+        try:
+            with sdrhip.Context(0) as ctx:
+                A = sdrhip.DeviceArray
+                I, Q = inputs[th]
+                d_I = [A.from_numpy(ctx, I[b]) for b in range(nblk)]
+                d_Q = [A.from_numpy(ctx, Q[b]) for b in range(nblk)]
+                d_out = [A(ctx, nstreams * nout * 4) for _ in range(nblk)]
+                d_h = A.from_numpy(ctx, h)
+                d_si, d_sq = A(ctx, nstreams * 400), A(ctx, nstreams * 400)
+                d_pi, d_pq = A(ctx, nstreams * 4), A(ctx, nstreams * 4)
+
+                def step(b):
+                    ctx.frontend_dev(D, d_I[b], d_Q[b], n, nstreams, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq,
+                                     d_out[b], nout)
+
+                def reset():
+                    for d in (d_si, d_sq, d_pi, d_pq):
+                        d.fill(0)
+
+                reset()
+                step(0)  # sizes the context's scratch before the capture
+                ctx.synchronize()
+                graph = ctx.capture(lambda: (step(1), step(2)))
+                barrier.wait()
+                for r in range(rounds):
+                    reset()
+                    for d in d_out:
+                        d.fill(0xFF)
+                    step(0)
+                    graph.launch()
+                    step(3)
+                    ctx.synchronize()
+                    want, states = wants[th]
+                    for b in range(nblk):
+                        assert_bits(d_out[b].download().reshape(nstreams, nout), want[b], f"thread {th} round {r} block {b}")
+                    assert_bits(d_si.download().reshape(nstreams, 100), np.stack([s[0] for s in states]), "state_i")
+                    assert_bits(d_sq.download().reshape(nstreams, 100), np.stack([s[1] for s in states]), "state_q")
+                    assert_bits(np.stack([d_pi.download(), d_pq.download()], 1), np.stack([s[2] for s in states]),
+                                "prev")
+                graph.close()
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append(f"thread {th}: {e!r}")
+            try:
+                barrier.abort()
+            except Exception:
+                pass
+
+    threads = [threading.Thread(target=worker, args=(th,)) for th in range(2)]
+    for t_ in threads:
+        t_.start()
+    for t_ in threads:
+        t_.join(timeout=100)
+    assert not any(t_.is_alive() for t_ in threads), "worker thread hung"
+    assert not errors, errors
+
+
+def test_dropin_two_threads_at_once(harness, oracle, tmp_path):
+    """Two host threads inside libdy4filter_hip.so concurrently (its context
+    pool leases one device context per call), each running its own stream's
+    block loop: front end + blockConvolveFIR per block, bitwise against the
+    oracle (src/project.cpp:299-302 is the reference's two-thread caller)."""
+    from sdrhip.synth import fm_iq_u8
+
+    D, block, nblk = 10, 51200, 8
+    h = oracle.taps_lpf(2.4e6, 100e3, 101, 1)
+    hb = oracle.taps_bpf(240e3, 18.5e3, 19.5e3, 101, 1)
+    iqs = [fm_iq_u8(block * nblk, seed=60 + t) for t in range(2)]
+    for t, iq in enumerate(iqs):
+        iq.tofile(tmp_path / f"iq{t}")
+    h.tofile(tmp_path / "h")
+    hb.tofile(tmp_path / "hb")
+    args = ["threads", D, tmp_path / "iq0", tmp_path / "iq1", tmp_path / "h", tmp_path / "hb", block, nblk,
+            tmp_path / "o0", tmp_path / "o1"]
+    r = subprocess.run([harness, *map(str, args)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    for t in range(2):
+        got = np.fromfile(tmp_path / f"o{t}", np.float32)
+        si, sq, sb, pv = (np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(100, np.float32),
+                          np.zeros(2, np.float32))
+        want = []
+        for b in range(nblk):
+            I, Q = oracle.u8_to_planar(iqs[t][2 * b * block:2 * (b + 1) * block])
+            dm = oracle.frontend(D, I, Q, h, si, sq, pv)
+            want += [dm, oracle.fir_block(dm, hb, sb)]
+        assert_bits(got, np.concatenate(want), f"thread {t}")
