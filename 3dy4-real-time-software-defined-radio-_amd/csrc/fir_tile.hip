@@ -30,6 +30,7 @@
 //     wave always has HBM reads in flight (software pipelining);
 //   * state carry: only the first tile of a stream reads `state`/`prev`;
 //     the workgroup that owns it rewrites them after its reads -- one kernel.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -50,6 +51,10 @@
 #ifndef SDR_NPASS
 #define SDR_NPASS 3
 #endif
+// SDR_FIR_DEFER: a tile's output stores wait until the next tile is staged
+#ifndef SDR_FIR_DEFER
+#define SDR_FIR_DEFER 1
+#endif
 // SDR_OUT_NT: non-temporal hint on the demod output stores of the f32 path
 // (warm same-box A/B: f32 -1..2 %, u8 neutral -> f32 only)
 #ifndef SDR_OUT_NT
@@ -57,10 +62,6 @@
 #endif
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
-#endif
-// SDR_IQ_PF: LDS chunk reads in flight ahead of the scan in fir_tile_iq
-#ifndef SDR_IQ_PF
-#define SDR_IQ_PF 3
 #endif
 
 namespace sdr {
@@ -73,9 +74,7 @@ __device__ __forceinline__ nf4 ldg_stream_n(const float4* p) {
   return *reinterpret_cast<const nf4*>(p);
 #endif
 }
-// a staged chunk as HIP's float4 (fir_tile) or the native vector (fir_tile_iq)
 __device__ __forceinline__ void set_chunk(float4& d, const nf4& v) { d = make_float4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ void set_chunk(nf4& d, const nf4& v) { d = v; }
 __device__ __forceinline__ uint2 ldg_stream(const uint2* p) {
 #if SDR_FIR_NT_U8
   typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -341,6 +340,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 // FMA = the fused multiply-add arithmetic mode (SDR_ARITH_FMA, SGPR taps
 // only): same taps, same order, one rounding per tap instead of two -- not
 // the reference's bits, within the fp32 tolerance of DESIGN.md 2.
+// fir_tile: one workgroup of NW waves per tile, the tiles walked statically
+// (walk 0: a contiguous run per workgroup; walk 1: XCD slabs, one tile per
+// workgroup in practice -- the dispatcher interleaves them).  The fused f32
+// front end's kernel: fir_tile_grp's persistent groups lost 13 % on cfg2
+// (DESIGN.md 5.2).
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
 __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __restrict__ h) {
   using G = Geom<D, T, R, DEMOD, NW>;
@@ -547,9 +551,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       float* o = a.out + (long long)tr.s * a.out_stride;
       // vector stores when the row keeps R-float groups aligned (uniform)
       const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
-      // ablate 3 (timing only): no output stores unless the result is a
-      // value it never is, so the scan still runs
-      if ((lane >= 1 || first) && (a.ablate != 3 || d[0] == 12345.0f)) {
+      if (lane >= 1 || first) {
         if (vec && m0 + R <= nout) {
           if constexpr (R == 2) {
             if constexpr (SDR_OUT_NT && SRC == Src::F32) {
@@ -675,277 +677,382 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
 }
 #undef SDR_TRACE_AT
 
-// ------------------------------------------------- I/Q-paired fused kernel --
-// fir_tile_iq: the fused front end (2 channels + discriminator) with I and Q
-// of each span position side by side in LDS, so one packed instruction
-// carries both channels: per tap and output
-//   v_pk_mul_f32 p, s[h_k pair] (op_sel broadcast of h_k), {I, Q}
-//   v_pk_add_f32 {accI, accQ}, {accI, accQ}, p
-// Each half is an IEEE single multiply and add rounded separately, exactly
-// the reference's two operations (src/filter.cpp:129-137): same bits as
-// fir_tile, half the FIR instructions, and the tap operand rides in the
-// SGPR pair the scalar loads already fill (no extra SGPRs).
-//
-// Layout: span position p holds {I, Q} at float index at(p) = 2p + 4*(p /
-// PADP).  PADP = D*R is the lane-window stride, so every lane's window
-// starts on a pad boundary and its chunk offsets are compile-time
-// constants; the 16-B pad makes the lane stride 44 dwords instead of 40,
-// which puts the 16 lanes of each ds_read_b128 group on 16 distinct 4-bank
-// slots (40 dwords give only 8: a 2-way conflict on every read).
-template <int D, int T, int R>
-struct IQGeom {
-  using G = Geom<D, T, R, true, 1>;
-  static constexpr int PADP = D * R;
-  static_assert(PADP % 4 == 0, "a staged 4-position chunk never straddles a pad");
-  static constexpr int LEN = 2 * G::LDS_LEN + 4 * ((G::LDS_LEN + PADP - 1) / PADP);
-  static constexpr int SMEM = LEN > 2 * G::STRIP ? LEN : 2 * G::STRIP;  // floats
-  static constexpr int LANE = 2 * PADP + 4;  // floats between adjacent lane windows
-  __device__ static __forceinline__ int at(int p) { return 2 * p + 4 * (p / PADP); }
-};
 
-// Tiles [first, last) by `step` this workgroup walks (see fir_tile).
-__device__ __forceinline__ void tile_walk(const FirLaunch& a, int total, int& first, int& step, int& last) {
-  if (a.walk == 0) {
-    first = blockIdx.x * a.tiles_per_wg;
-    step = 1;
-    last = min(first + a.tiles_per_wg, total);
-  } else {
-    const int per_xcd = (total + 7) / 8;
-    const int x = blockIdx.x & 7;
-    step = gridDim.x >> 3;
-    first = x * per_xcd + (blockIdx.x >> 3);
-    last = min((x + 1) * per_xcd, total);
-  }
+// A wave's own LDS slice is published to its other lanes: LDS operations of
+// one wave execute in order, so the wait and a compiler barrier suffice (the
+// workgroup's other waves work on other tiles and are never waited for).
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
 }
 
-template <int D, int T, int R, Src SRC, bool FMA = false>
-__global__ __launch_bounds__(64) void fir_tile_iq(FirLaunch a, const float* __restrict__ h) {
-  using G = Geom<D, T, R, true, 1>;
-  using P = IQGeom<D, T, R>;
-  constexpr int NW = 1, NCH = 2;
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef float f4 __attribute__((ext_vector_type(4)));
+// Launch shape: persistent workgroups (a group each, one or two per CU),
+// blockDim.x / 64 waves each.  Every wave owns one LDS slice of G::SMEM
+// floats and works through the group's tiles on its own, claiming the next
+// one from a counter in LDS when its staging is done, so the waves on a
+// lightly loaded SIMD take more tiles than those sharing a SIMD with more
+// waves.  The group's k-th claim is tile  slab + j + k * groups_per_slab
+// (walk 1: group g = 8j + x works in XCD slab x, a contiguous eighth of the
+// tiles; walk 0: one slab): the chip streams through a contiguous window of
+// each slab, as one workgroup per tile dispatched in order did, and a
+// tile's halo -- its neighbour's tail -- is read in the same XCD's L2 (round
+// robin placement; speed only).  One workgroup per tile, the round-2 shape,
+// left a CU with 10-11 of its 14 workgroup slots occupied on average:
+// workgroup dispatch, not HBM, set the rate (tools/fir_trace.py); a static
+// persistent walk lost the difference in its tail; giving each group a
+// contiguous run of tiles instead (256 separate read cursors) cost 13 % on
+// cfg2.
+#ifndef SDR_FIR_LB
+#define SDR_FIR_LB 1024
+#endif
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
+__global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const float* __restrict__ h) {
+  using G = Geom<D, T, R, DEMOD, NW>;
+  constexpr int NTH = G::NTH;
+  static_assert(NW == 1, "one wave per tile");
+  static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
+  static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
+  static_assert(TM == 1, "taps as SGPR operands");
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* strip0 = smem;  // tile 0, after its scan: the block's last inputs, planar
-  float* strip1 = smem + G::STRIP;
+  __shared__ int next_tile;  // the group's claim counter
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* lds0 = smem + wv * G::SMEM;  // this wave's slice
+  float* lds1 = lds0 + G::LDS_LEN;
+  float* strip0 = lds0;  // the block's last inputs (tile 0, after its scan)
+  float* strip1 = lds1;
 
-  const int tid = threadIdx.x;
-  const int lane = tid;
+  const int tid = threadIdx.x & 63;
+  const int lane = tid, wave = 0;
   const long long n = a.n;
   const long long nout = n / D;
   const int ns = a.ns;
-  int first, step, last;
-  tile_walk(a, a.nstreams * a.tiles_per_stream, first, step, last);
-  if (first >= last) return;
+  const int total = a.nstreams * a.tiles_per_stream;
+  // group b: slab x = b % 8 (walk 1; workgroups are dealt to the XCDs round
+  // robin, so a slab's groups share an L2: speed only), the j-th run of
+  // a.tiles_per_wg consecutive tiles in it
+  // the group's k-th tile is slab start + j + k * (groups per slab): all
+  // groups of a slab advance through one window of it (a.walk: 8 slabs)
+  const int sh = a.walk ? 3 : 0;
+  const int x = blockIdx.x & ((1 << sh) - 1), j = blockIdx.x >> sh, gps = gridDim.x >> sh;
+  const int s_lo = x * a.slab, s_hi = min(s_lo + a.slab, total);
+  if (threadIdx.x == 0) next_tile = 0;
+  __syncthreads();  // the only workgroup barrier
+  // one LDS atomic per claim (lgkmcnt: never waits on vector memory)
+  auto claim = [&]() __attribute__((always_inline)) {
+    int v = 0;
+    if (tid == 0) v = atomicAdd(&next_tile, 1);
+    v = s_lo + j + __builtin_amdgcn_readfirstlane(v) * gps;
+    return v < s_hi ? v : -1;
+  };
+  const int first = claim();
+  if (first < 0) return;
+#ifdef SDR_FIR_TRACE
+  unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime();
+#define SDR_TRACE_AT(i)                                        \
+  {                                                            \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    if ((i) > 0) tr_sum[(i) - 1] += now_ - tr_last;            \
+    tr_last = now_;                                            \
+  }
+#else
+#define SDR_TRACE_AT(i)
+#endif
 
-  using Stage = f4[G::FULL + 1];
+  using Stage = float4[G::FULL + 1];
   Stage sa0, sa1;
 #pragma unroll
-  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.ablate != 1)
-    stage_load<D, T, R, true, NW, NCH, SRC>(tile_ref<D, T, R, true, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
+    stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
 
-  auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
-    const TileRef tr = tile_ref<D, T, R, true, NW, NCH, SRC>(a, lin);
-    float old_pi = 0.0f, old_pq = 0.0f;
-    if (tr.t == 0) {  // workgroup-uniform; scalar loads (see fir_tile)
-      using cf = const __attribute__((address_space(4))) float*;
-      const int s = __builtin_amdgcn_readfirstlane(tr.s);
-      old_pi = ((cf)a.prev0)[s];
-      old_pq = ((cf)a.prev1)[s];
-    }
-
-    // ---- 1. registers -> LDS, I/Q interleaved; prefetch the next tile
-    __syncthreads();
-    {
-      auto put = [&](int i, const f4& a0, const f4& a1) {
-        float* d = smem + P::at(4 * i);
-        if constexpr (SRC == Src::U8) {
-          // 8 wire bytes = I0 Q0 I1 Q1 | I2 Q2 I3 Q3: already the pair order
-          const uint32_t bx = __float_as_uint(a0.x), by = __float_as_uint(a0.y);
-          *reinterpret_cast<f4*>(d) = f4{u8_byte_to_f32<0>(bx), u8_byte_to_f32<1>(bx), u8_byte_to_f32<2>(bx),
-                                         u8_byte_to_f32<3>(bx)};
-          *reinterpret_cast<f4*>(d + 4) = f4{u8_byte_to_f32<0>(by), u8_byte_to_f32<1>(by), u8_byte_to_f32<2>(by),
-                                             u8_byte_to_f32<3>(by)};
-        } else {
-          // whole-vector shuffles of native vectors (element access of HIP
-          // float4s here pushed the stage arrays to scratch)
-          *reinterpret_cast<f4*>(d) = __builtin_shufflevector(a0, a1, 0, 4, 1, 5);
-          *reinterpret_cast<f4*>(d + 4) = __builtin_shufflevector(a0, a1, 2, 6, 3, 7);
-        }
-      };
+  // A tile's outputs wait in registers and are stored after the next tile's
+  // loads have been waited for: stored at the end of their own tile, they
+  // were the youngest vector-memory operations when the next tile's staging
+  // waited (vmcnt counts loads and stores in issue order), so every tile paid
+  // its stores' write latency on top of its loads'.
+  float pend[R];
+  float* pend_row = nullptr;
+  long long pend_m0 = nout;  // nout: nothing pending in this lane
+  bool pend_vec = false;
+  auto flush = [&]() __attribute__((always_inline)) {
+    float* o = pend_row;
+    if (pend_vec && pend_m0 + R <= nout) {
+      if constexpr (R == 2) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        if constexpr (SDR_OUT_NT && SRC == Src::F32 && DEMOD)
+          __builtin_nontemporal_store(f2{pend[0], pend[1]}, reinterpret_cast<f2*>(o + pend_m0));
+        else
+          *reinterpret_cast<f2*>(o + pend_m0) = f2{pend[0], pend[1]};
+      } else if constexpr (R == 4) {
+        *reinterpret_cast<float4*>(o + pend_m0) = make_float4(pend[0], pend[1], pend[2], pend[3]);
+      } else {
 #pragma unroll
-      for (int it = 0; it < G::FULL; ++it) put(tid + it * G::NTH, v0[it], v1[it]);
-      if (G::REM && tid < G::REM) put(tid + G::FULL * G::NTH, v0[G::FULL], v1[G::FULL]);
+        for (int r = 0; r < R; ++r) o[pend_m0 + r] = pend[r];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (pend_m0 + r < nout) o[pend_m0 + r] = pend[r];
     }
-    if (tr.t == 0 || !interior<D, T, R, true, NW>(tr, n)) {  // workgroup-uniform
-      __syncthreads();
-      edge_fill<D, T, R, true, NW, NCH, SRC>(tr, tid, n, ns, [&](int i, float e0, float e1) {
-        *reinterpret_cast<f2*>(smem + P::at(i)) = f2{e0, e1};
+    pend_m0 = nout;
+  };
+  // nxt(): the tile to prefetch after this one's staging (-1: none)
+  auto tile = [&](const int lin, auto&& nxt, Stage& v0, Stage& v1) __attribute__((always_inline)) {
+    const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin);
+    // Old prev_I/prev_Q, read before this workgroup rewrites them at the
+    // end of the iteration (tile 0 only).
+    float old_pi = 0.0f, old_pq = 0.0f;
+    if constexpr (DEMOD) {
+      // scalar loads (lgkmcnt, not vmcnt): a conditional vector load here
+      // makes the waitcnt pass drain the prefetch queue at the scan.  The
+      // value is the launch's input: only this workgroup rewrites it, after
+      // this read.
+      if (tr.t == 0) {  // workgroup-uniform
+        using cf = const __attribute__((address_space(4))) float*;
+        const int s = __builtin_amdgcn_readfirstlane(tr.s);
+        old_pi = ((cf)a.prev0)[s];
+        old_pq = ((cf)a.prev1)[s];
+      }
+    }
+
+    // ---- 1. registers -> LDS (after every read of the previous tile), then
+    // prefetch the next tile into the registers just freed.  Tile 0 also
+    // stages the block's last STRIP inputs (old state where p < 0: the
+    // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
+    // rewrites the state below.
+    SDR_TRACE_AT(0);
+    wave_sync();
+#ifdef SDR_FIR_TRACE
+    __builtin_amdgcn_s_waitcnt(0);
+    SDR_TRACE_AT(1);
+#endif
+    stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
+    if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
+      wave_sync();
+      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, [&](int i, float v0, float v1) {
+        lds0[i] = v0;
+        if (NCH == 2) lds1[i] = v1;
       });
     }
-    __syncthreads();
-    if (lin + step < last && a.ablate != 1)
-      stage_load<D, T, R, true, NW, NCH, SRC>(tile_ref<D, T, R, true, NW, NCH, SRC>(a, lin + step), n, tid, v0, v1);
+    wave_sync();
+    SDR_TRACE_AT(2);
+    const int next = nxt();
+    if constexpr (SDR_FIR_DEFER) flush();  // the previous tile's outputs
+    if (next >= 0 && a.ablate != 1)
+      stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, next), n, tid, v0, v1);
 
-    // ---- 2. the lane's window: chunk c = positions 2c, 2c+1 = {I, Q, I, Q}
-    f2 acc[R];
+    // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
+    // Lane (wave, lane) owns outputs m_start + wave*WADV + R*lane + r.  Per
+    // 4-position chunk c it reads NCH input float4s of its own window; the
+    // next chunk is prefetched, and the sched_barrier keeps the scheduler from
+    // hoisting every LDS read of the unrolled loop (registers -> occupancy).
+    const int lbase = D * (wave * G::WADV + R * lane);  // LDS index of this lane's window
+    float acc0[R], acc1[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = f2{0.0f, 0.0f};
-    const float* w = smem + P::LANE * lane;
+    for (int r = 0; r < R; ++r) {
+      acc0[r] = 0.0f;
+      acc1[r] = 0.0f;
+    }
     if (a.ablate == 2) {
-      acc[0] = *reinterpret_cast<const f2*>(w);
+      acc0[0] = lds0[lbase];
+      acc1[0] = lds1[lbase];
     } else {
-      // taps as SGPR pairs {h_k, h_k+1}, NPASS passes over consecutive tap
-      // ranges (every output still visits k = 0..T-1 in order)
-      constexpr int NPASS = SDR_NPASS, KP = ((T + NPASS - 1) / NPASS + 1) / 2 * 2;
-      using hconst = const __attribute__((address_space(4))) float*;
-      const hconst hc = (hconst)h;
-      f2 hp[KP / 2];
-      static_for<0, NPASS>([&](auto pi) {
-        constexpr int k0 = decltype(pi)::value * KP;
-        constexpr int k1 = k0 + KP < T ? k0 + KP : T;
-        if constexpr (k0 < T) {
+      const float* w0 = lds0 + lbase;
+      const float* w1 = lds1 + lbase;
+      {
+        // Taps as SGPR operands of the multiplies: no LDS tap traffic.  All
+        // T taps do not fit the SGPR file beside the addressing, so the
+        // window is walked in NPASS passes over consecutive tap ranges
+        // [k0, k1), each loading its taps once (scalar loads from the
+        // constant address space, one wait) -- every output still visits
+        // k = 0..T-1 in order, the passes only split its chain.
+        constexpr int NPASS = SDR_NPASS, KP = (T + NPASS - 1) / NPASS;
+        using hconst = const __attribute__((address_space(4))) float*;
+        const hconst hc = (hconst)h;
+        float hs[KP];
+        static_for<0, NPASS>([&](auto pi) {
+          constexpr int k0 = decltype(pi)::value * KP;
+          constexpr int k1 = k0 + KP < T ? k0 + KP : T;
+          // ablate 4 (timing only): one pass of three -- how much a cheaper scan buys
           if (a.ablate == 4 && k0 > 0) return;
 #pragma unroll
-          for (int i = 0; i < (k1 - k0 + 1) / 2; ++i)
-            hp[i] = f2{hc[k0 + 2 * i], k0 + 2 * i + 1 < k1 ? hc[k0 + 2 * i + 1] : 0.0f};
+          for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
 #pragma unroll
-          for (int i = 0; i < (k1 - k0 + 1) / 2; ++i) asm volatile("" : "+s"(hp[i]));
+          for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
+          // window positions w = HALO + D r - k this pass touches
           constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
           constexpr int whi = G::HALO + D * (R - 1) - k0;
-          constexpr int clo = wlo / 2, chi = whi / 2;
-          auto chunk = [&](int c) { return *reinterpret_cast<const f4*>(w + 4 * c + 4 * ((2 * c) / P::PADP)); };
-          // LDS reads PF chunks ahead: a chunk is only ~8 packed
-          // instructions of work, far shorter than an LDS read's latency
-          constexpr int PF = SDR_IQ_PF, NB = PF + 1;
-          f4 buf[NB];
-          static_for<0, PF>([&](auto pi2) {
-            constexpr int c = chi - decltype(pi2)::value;
-            if constexpr (c >= clo) buf[c % NB] = chunk(c);
-          });
+          constexpr int clo = wlo / 4, chi = whi / 4;
+          float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * chi);
+          float4 q1 = q0;
+          if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * chi);
           static_for<0, chi - clo + 1>([&](auto ci) {
             constexpr int c = chi - decltype(ci)::value;
-            if constexpr (c - PF >= clo) buf[(c - PF) % NB] = chunk(c - PF);
-            const f4 q = buf[c % NB];
-            const f2 e[2] = {f2{q.x, q.y}, f2{q.z, q.w}};
-            static_for<0, 2>([&](auto ji) {
-              constexpr int j = 1 - decltype(ji)::value;
+            float4 n0 = q0, n1 = q1;
+            if constexpr (c > clo) {
+              n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
+              if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+            }
+            const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+            const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+            static_for<0, 4>([&](auto ji) {
+              constexpr int j = 3 - decltype(ji)::value;
               static_for<0, R>([&](auto ri) {
                 constexpr int r = decltype(ri)::value;
-                constexpr int k = G::HALO + D * r - (2 * c + j);
+                constexpr int k = G::HALO + D * r - (4 * c + j);
                 if constexpr (k >= k0 && k < k1) {
-                  const float hk = ((k - k0) & 1) ? hp[(k - k0) / 2].y : hp[(k - k0) / 2].x;
-                  if constexpr (FMA)
-                    acc[r] = __builtin_elementwise_fma(f2{hk, hk}, e[j], acc[r]);
-                  else
-                    acc[r] = acc[r] + f2{hk, hk} * e[j];
+                  if constexpr (FMA) {
+                    acc0[r] = __builtin_fmaf(hs[k - k0], e0[j], acc0[r]);
+                    if (NCH == 2) acc1[r] = __builtin_fmaf(hs[k - k0], e1[j], acc1[r]);
+                  } else {
+                    acc0[r] = acc0[r] + hs[k - k0] * e0[j];
+                    if (NCH == 2) acc1[r] = acc1[r] + hs[k - k0] * e1[j];
+                  }
                 }
               });
             });
+            q0 = n0;
+            q1 = n1;
 #pragma unroll
-            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+            for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
             __builtin_amdgcn_sched_barrier(0);
           });
-        }
-      });
+        });
+      }
     }
 
-    // ---- 3. discriminator in registers (as fir_tile)
-    const long long m0 = tr.m_start + (long long)R * lane;
-    {
-      float pI = __shfl_up(acc[R - 1].x, 1, 64);
-      float pQ = __shfl_up(acc[R - 1].y, 1, 64);
-      const bool first_out = tr.t == 0 && tid == 0;
-      if (first_out) {
+    SDR_TRACE_AT(3);
+    // ---- 3. the tile's outputs, kept in registers (pend) and stored after
+    // the NEXT tile's staging -- see flush()
+    const long long m0 = tr.m_start + (long long)wave * G::WADV + (long long)R * lane;  // this lane's first output
+    if constexpr (DEMOD) {
+      // discriminator in registers.  The decimated sample before output r=0
+      // is lane-1's last output (a wave shuffle); lane 0's outputs are the
+      // wave's overlap and are not stored, except at the start of the stream
+      // (tile 0, wave 0, lane 0 -> outputs 0..R-1), whose predecessor is the
+      // carried prev_*.
+      float pI = __shfl_up(acc0[R - 1], 1, 64);
+      float pQ = __shfl_up(acc1[R - 1], 1, 64);
+      const bool first = tr.t == 0 && tid == 0;
+      if (first) {
         pI = old_pi;
         pQ = old_pq;
       }
-      float d[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const float ip = r ? acc[r - 1].x : pI;
-        const float qp = r ? acc[r - 1].y : pQ;
-        d[r] = demod_one(acc[r].x, acc[r].y, ip, qp);
+        const float ip = r ? acc0[r - 1] : pI;
+        const float qp = r ? acc1[r - 1] : pQ;
+        pend[r] = demod_one(acc0[r], acc1[r], ip, qp);
       }
-      float* o = a.out + (long long)tr.s * a.out_stride;
-      const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
-      if ((lane >= 1 || first_out) && (a.ablate != 3 || d[0] == 12345.0f)) {
-        if (vec && m0 + R <= nout) {
-          if constexpr (R == 2) {
-            if constexpr (SDR_OUT_NT && SRC == Src::F32)
-              __builtin_nontemporal_store(f2{d[0], d[1]}, reinterpret_cast<f2*>(o + m0));
-            else
-              *reinterpret_cast<f2*>(o + m0) = f2{d[0], d[1]};
-          } else if constexpr (R == 4) {
-            *reinterpret_cast<f4*>(o + m0) = f4{d[0], d[1], d[2], d[3]};
-          } else {
+      pend_row = a.out + (long long)tr.s * a.out_stride;
+      pend_m0 = (lane >= 1 || first) ? m0 : nout;  // lane 0 of a later tile: recomputed overlap, not stored
+    } else {
 #pragma unroll
-            for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (m0 + r < nout) o[m0 + r] = d[r];
-        }
-      }
+      for (int r = 0; r < R; ++r) pend[r] = acc0[r];
+      pend_row = a.y0 + (long long)tr.s * a.y_stride;
+      pend_m0 = m0;
     }
+    // vector stores when the row keeps R-float groups aligned (uniform)
+    pend_vec = ((reinterpret_cast<uintptr_t>(pend_row) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+    if constexpr (!SDR_FIR_DEFER) flush();
 
-    // ---- 4. state carry (tile 0 only), planar strips as in fir_tile
+    // ---- 4. state carry (tile 0 only; every read of the old values
+    // happened before the barriers above)
     if (tr.t == 0) {
-      __syncthreads();
-      for (int j0 = 0; j0 < G::STRIP; j0 += 4 * G::NTH) {
-        float s0[4], s1[4];
+      // stage the block's last STRIP inputs (old state where p < 0: the
+      // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) into the
+      // channel buffers, free once every lane's scan has read them
+      wave_sync();
+      for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
+        float v0[4], v1[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int j = j0 + u * G::NTH + tid;
+          const int j = j0 + u * NTH + tid;
           const long long p = n - G::STRIP + j;
-          s0[u] = s1[u] = 0.0f;
+          v0[u] = v1[u] = 0.0f;
           if (j < G::STRIP) {
-            s0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
-            s1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
+            v0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
+            if (NCH == 2) v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
           }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int j = j0 + u * G::NTH + tid;
+          const int j = j0 + u * NTH + tid;
           if (j < G::STRIP) {
-            strip0[j] = s0[u];
-            strip1[j] = s1[u];
+            strip0[j] = v0[u];
+            if (NCH == 2) strip1[j] = v1[u];
           }
         }
       }
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      // prev_* <- last decimated I/Q (src/filter.cpp:100-101), reference order
-      if (tid < 2) {
-        using hconst = const __attribute__((address_space(4))) float*;
-        const hconst hc = (hconst)h;
-        const float* sp = (tid == 0 ? strip0 : strip1) + (G::STRIP - D);
-        float y = 0.0f;
+      __builtin_amdgcn_s_waitcnt(0);  // as in edge_fill: keep the waitcnt pass from draining at the next scan
+      wave_sync();
+      if constexpr (DEMOD) {
+        // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
+        // recomputed in the reference's order from the staged strip:
+        // input D*(nout-1) - k = n - D - k sits at strip index STRIP - D - k
+        // (lane c < 2 runs channel c; groups of 8 LDS reads in flight -- a
+        // full unroll would hold all T reads live and cost a wave per SIMD
+        // of occupancy for the whole kernel)
+        if (tid < 2) {
+          using hconst = const __attribute__((address_space(4))) float*;
+          const hconst hc = (hconst)h;
+          const float* sp = (tid == 0 ? strip0 : strip1) + (G::STRIP - D);
+          float y = 0.0f;
 #pragma unroll 8
-        for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
-        (tid == 0 ? a.prev0 : a.prev1)[tr.s] = y;
+          for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
+          (tid == 0 ? a.prev0 : a.prev1)[tr.s] = y;
+        }
       }
       // state <- last ns input samples (src/filter.cpp:139)
       if (ns <= G::STRIP) {
-        for (int j = tid; j < ns; j += G::NTH) {
+        for (int j = tid; j < ns; j += NTH) {
           tr.st0[j] = strip0[G::STRIP - ns + j];
-          tr.st1[j] = strip1[G::STRIP - ns + j];
+          if (NCH == 2) tr.st1[j] = strip1[G::STRIP - ns + j];
         }
       } else {
-        for (int j = tid; j < ns; j += G::NTH) {
+        for (int j = tid; j < ns; j += NTH) {
           const long long p = n - ns + j;
           tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, p);
-          tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
+          if (NCH == 2) tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, p);
         }
       }
     }
   };
 
-  for (int lin = first; lin < last; lin += step) tile(lin, sa0, sa1);
+#ifdef SDR_FIR_TRACE
+#define SDR_TRACE_TILE() \
+  SDR_TRACE_AT(4);       \
+  ++tr_n
+#else
+#define SDR_TRACE_TILE()
+#endif
+  for (int lin = first; lin >= 0;) {
+    int next = -1;
+    tile(lin, [&]() __attribute__((always_inline)) {
+      next = claim();
+      return next;
+    }, sa0, sa1);
+    SDR_TRACE_TILE();
+    lin = next;
+  }
+  flush();
+#undef SDR_TRACE_TILE
+#ifdef SDR_FIR_TRACE
+  if (tid == 0 && blockIdx.x * 16 + wv < kTraceWG) {  // one record per wave
+    unsigned long long* o = g_fir_trace + 8ull * (blockIdx.x * 16 + wv);
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    o[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    o[1] = tr_r0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[2 + i] = tr_sum[i];
+    o[6] = tr_n;
+    o[7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
+#undef SDR_TRACE_AT
 
 // ---------------------------------------------------------- generic path --
 // Any D / T / ns the tiled kernel is not instantiated for.  One thread per
@@ -1018,23 +1125,52 @@ __global__ __launch_bounds__(kWG) void demod_kernel(const float* I, const float*
 }
 
 // ------------------------------------------------------------ dispatch ----
-// Persistent grid: about `wpc` waves per CU (or the tile count, if smaller),
-// each workgroup walking its share of the tiles (see `walk` in fir_tile).
-template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false, bool IQ = false>
-hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc) {
+// persist = false: fir_tile, about `wpc` one-wave workgroups per CU
+// requested (64 for the fused f32 front end: one tile each),
+// walking XCD slabs.  persist = true: fir_tile_grp, one workgroup per CU (or
+// as many as LDS and 32 waves allow) of as many waves as the CU's LDS holds
+// slices (<= 16: the 4 waves per SIMD that <= 128 VGPRs allow), the groups
+// claiming interleaved tiles of XCD slabs.
+template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
+hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool persist, int wpc) {
   using G = Geom<D, T, R, DEMOD, NW>;
   FirLaunch a = a0;
   const long long nout = a.n / D;
   a.tiles_per_stream = nout > G::E ? (int)((nout - G::E + G::ADV - 1) / G::ADV) : 1;
   const long long total = (long long)a.tiles_per_stream * a.nstreams;
   if (total <= 0 || total > 0x7fffffffLL) return hipErrorInvalidValue;
-  const int ncu = device_cu_count();
+  const long long ncu = device_cu_count();
+  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
+  a.ablate = ablate;
+  static const int persist_env = env_int("SDR_FIR_PERSIST", -1);  // A/B
+  if (persist_env >= 0) persist = persist_env != 0;
+  if (persist) {
+    constexpr long long kLds = 163840 - 64;  // a CU's LDS, less the claim counter
+    constexpr long long slice = (long long)G::SMEM * sizeof(float);
+    static const int wpg_env = env_int("SDR_FIR_WPG", 0);  // timing experiments
+    long long wpg = std::min<long long>(16, kLds / slice);
+    if (wpg_env > 0) wpg = std::min<long long>(wpg, wpg_env);
+    const long long wg_per_cu = std::max<long long>(1, std::min<long long>(32 / wpg, kLds / (wpg * slice)));
+    long long groups = std::min<long long>(ncu * wg_per_cu, (total + wpg - 1) / wpg);
+    if (total >= 64 && groups >= 8) {
+      groups -= groups % 8;
+      a.walk = 1;
+      a.slab = (int)((total + 7) / 8);
+    } else {
+      a.walk = 0;
+      a.slab = (int)total;
+    }
+    const long long per = (a.slab + (groups >> (a.walk ? 3 : 0)) - 1) / (groups >> (a.walk ? 3 : 0));
+    wpg = std::max<long long>(1, std::min<long long>(wpg, per));
+    hipLaunchKernelGGL((fir_tile_grp<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)groups),
+                       dim3((unsigned)(64 * wpg)), (size_t)(wpg * slice), st, a, h);
+    return hipGetLastError();
+  }
   static const int per_cu_env = env_int("SDR_WG_PER_CU", 0);
   const int per_cu = per_cu_env > 0 ? per_cu_env : wpc;
-  static const int walk = env_int("SDR_TILE_WALK", 1);
-  const long long slots = (long long)ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
+  const long long slots = ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
   long long blocks;
-  if (walk == 1 && total >= 8 * 8) {
+  if (total >= 8 * 8) {
     // a multiple of 8 workgroups, none of them idle
     a.walk = 1;
     const long long per_xcd = (total + 7) / 8;
@@ -1047,17 +1183,9 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
     a.tiles_per_wg = (int)((total + grid - 1) / grid);
     blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
   }
-  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
-  a.ablate = ablate;
-  if constexpr (IQ) {
-    static_assert(NW == 1 && NCH == 2 && DEMOD, "the I/Q-paired kernel is the fused one-wave front end");
-    const size_t lds = (size_t)IQGeom<D, T, R>::SMEM * sizeof(float);
-    hipLaunchKernelGGL((fir_tile_iq<D, T, R, SRC, FMA>), dim3((unsigned)blocks), dim3(64), lds, st, a, h);
-  } else {
-    const size_t lds = (size_t)G::SMEM * sizeof(float);
-    hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds,
-                       st, a, h);
-  }
+  const size_t lds = (size_t)G::SMEM * sizeof(float);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st,
+                     a, h);
   return hipGetLastError();
 }
 
@@ -1066,18 +1194,17 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, int wpc
 // be a multiple of 4 (aligned lane windows).  These are the measured best on
 // MI355X (where the variants that lost are listed).
 struct Variant {
-  int R, NW, tm, wpc;
+  int R, NW, tm;
 };
 
 Variant variant_for(int D, bool demod, Src src) {
   switch (D) {
-    // f32 fused: 64 one-wave workgroups per CU
-    case 10: return src == Src::F32 && demod ? Variant{2, 1, 1, 64} : Variant{2, 1, 1, 32};
-    case 5: return {4, 1, 1, 32};
+    case 10: return {2, 1, 1};
+    case 5: return {4, 1, 1};
     // D = 1 (the band-pass filters): SGPR taps too -- 31.4 vs 37.8 us per
     // 1,024 x 5,120 block against LDS tap rows (scripts/d1bench.py)
-    case 1: return {4, 1, 1, 32};
-    default: return {0, 0, 0, 32};
+    case 1: return {4, 1, 1};
+    default: return {0, 0, 0};
   }
 }
 
@@ -1094,34 +1221,27 @@ bool geometry_ok(int D, int T, int ns, bool demod, Variant v) {
 template <int NCH, bool DEMOD, Src SRC>
 hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, bool* handled) {
   *handled = true;
-  const Variant v = variant_for(a.D, DEMOD, SRC);
+  constexpr bool kPersistFused = SRC == Src::U8;
   if (a.ntaps == 101) {
     if constexpr (DEMOD) {
       // SDR_ARITH_FMA: instantiated for the fused kernels; any other shape
       // runs the exact arithmetic (inside the tolerance)
-      // SDR_FIR_IQ=1 (A/B only): the I/Q-paired packed kernel instead of
-      // the planar one (same bits; 8 % slower on cfg2)
-      static const bool iq = env_int("SDR_FIR_IQ", 0) != 0;
       switch (a.D) {
+        // the u8 wire format (VALU-bound: 2.4 B per pair) runs persistent
+        // groups; f32 (HBM-bound) one tile per workgroup -- DESIGN.md 5.2
         case 10:
-          if (iq)
-            return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true, true>(a, h, st, v.wpc)
-                         : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, false, true>(a, h, st, v.wpc);
-          return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, v.wpc)
-                       : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+          return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 64)
+                       : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, kPersistFused, 64);
         case 5:
-          if (iq)
-            return a.fma ? run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, true, true>(a, h, st, v.wpc)
-                         : run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, false, true>(a, h, st, v.wpc);
-          return a.fma ? run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, v.wpc)
-                       : run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+          return a.fma ? run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 32)
+                       : run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, kPersistFused, 32);
         default: break;
       }
     } else if constexpr (NCH == 1) {
       switch (a.D) {
-        case 10: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 5: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
-        case 1: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, v.wpc);
+        case 10: return run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, true, 32);
+        case 5: return run_tile<5, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, true, 32);
+        case 1: return run_tile<1, 101, 4, 1, NCH, DEMOD, SRC, 1>(a, h, st, true, 32);
         default: break;
       }
     }

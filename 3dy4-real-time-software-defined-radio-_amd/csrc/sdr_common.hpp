@@ -41,9 +41,10 @@ struct FirLaunch {
   float* out;
   long long out_stride;
   int tiles_per_stream;
-  int tiles_per_wg;  // persistent tile kernels: tiles per workgroup
-  int walk;          // 0: each workgroup walks contiguous tiles; 1: XCD-strided (see fir_tile.hip)
-  int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math, 3 = no output stores
+  int tiles_per_wg;  // fir_tile: tiles per workgroup (see fir_tile.hip)
+  int walk;          // fir_tile: 0 a run per workgroup, 1 XCD slabs; fir_tile_grp: 1 XCD slabs, 0 one slab
+  int slab;          // fir_tile_grp: tiles per slab
+  int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math, 4 = one tap pass of three
   int fma;           // SDR_ARITH_FMA: fused multiply-add FIR arithmetic where a fast path implements it
 };
 
