@@ -52,6 +52,11 @@
 #define SDR_NPASS 3
 #endif
 // SDR_FIR_DEFER: a tile's output stores wait until the next tile is staged
+// SDR_SCAN_PF: chunks of a lane's window read from LDS ahead of the chunk
+// being multiplied (its lgkmcnt wait covers the rest)
+#ifndef SDR_SCAN_PF
+#define SDR_SCAN_PF 1
+#endif
 #ifndef SDR_FIR_DEFER
 #define SDR_FIR_DEFER 1
 #endif
@@ -488,16 +493,24 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
           constexpr int whi = G::HALO + D * (R - 1) - k0;
           constexpr int clo = wlo / 4, chi = whi / 4;
-          float4 q0 = *reinterpret_cast<const float4*>(w0 + 4 * chi);
-          float4 q1 = q0;
-          if (NCH == 2) q1 = *reinterpret_cast<const float4*>(w1 + 4 * chi);
+          // SDR_SCAN_PF chunks of LDS reads in flight ahead of the one in use
+          constexpr int PF = SDR_SCAN_PF;
+          float4 pf0[PF + 1], pf1[PF + 1];
+          static_for<0, PF>([&](auto ui) {
+            constexpr int u = decltype(ui)::value;
+            if constexpr (chi - u >= clo) {
+              pf0[u] = *reinterpret_cast<const float4*>(w0 + 4 * (chi - u));
+              pf1[u] = pf0[u];
+              if (NCH == 2) pf1[u] = *reinterpret_cast<const float4*>(w1 + 4 * (chi - u));
+            }
+          });
           static_for<0, chi - clo + 1>([&](auto ci) {
             constexpr int c = chi - decltype(ci)::value;
-            float4 n0 = q0, n1 = q1;
-            if constexpr (c > clo) {
-              n0 = *reinterpret_cast<const float4*>(w0 + 4 * (c - 1));
-              if (NCH == 2) n1 = *reinterpret_cast<const float4*>(w1 + 4 * (c - 1));
+            if constexpr (c - PF >= clo) {
+              pf0[PF] = *reinterpret_cast<const float4*>(w0 + 4 * (c - PF));
+              if (NCH == 2) pf1[PF] = *reinterpret_cast<const float4*>(w1 + 4 * (c - PF));
             }
+            const float4 q0 = pf0[0], q1 = NCH == 2 ? pf1[0] : pf0[0];
             const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
             const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
             static_for<0, 4>([&](auto ji) {
@@ -516,8 +529,11 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
                 }
               });
             });
-            q0 = n0;
-            q1 = n1;
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+              pf0[u] = pf0[u + 1];
+              pf1[u] = pf1[u + 1];
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
             __builtin_amdgcn_sched_barrier(0);
@@ -1152,6 +1168,9 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
     if (wpg_env > 0) wpg = std::min<long long>(wpg, wpg_env);
     const long long wg_per_cu = std::max<long long>(1, std::min<long long>(32 / wpg, kLds / (wpg * slice)));
     long long groups = std::min<long long>(ncu * wg_per_cu, (total + wpg - 1) / wpg);
+    // timing experiments: about k tiles per wave, as many groups as that takes
+    static const int wave_tiles = env_int("SDR_FIR_WAVE_TILES", 0);
+    if (wave_tiles > 0) groups = std::max<long long>(8, (total + wpg * wave_tiles - 1) / (wpg * wave_tiles) + 7);
     if (total >= 64 && groups >= 8) {
       groups -= groups % 8;
       a.walk = 1;
