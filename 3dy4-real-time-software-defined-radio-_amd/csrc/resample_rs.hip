@@ -403,8 +403,11 @@ __global__ __launch_bounds__(kLpSlots) void build_lp_tables(const float* __restr
 // Stage item `it` (its whole input span) into buf: LDS-DMA for the chunks
 // inside [0, n), registers for the chunks that reach into the carried state
 // or past the end.
+// The staging threads: tid of nth, in waves wv of nwv (all of the compute
+// waves, or the one loader wave).
 template <int CMAX>
-__device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, int wv, int ln) {
+__device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, int tid, int nth, int wv, int nwv,
+                                         int ln) {
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
   const int st = it / a.nbat, b = it - st * a.nbat;
   const int t0 = b * a.C;
@@ -420,7 +423,6 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
   if (jhi > nch) jhi = nch;
   // edges first (chunks below jlo and from jhi up): their register loads then
   // do not wait behind this item's DMAs
-  const int tid = threadIdx.x;
   auto edge = [&](int j) {
     const long long g = P0 + 4LL * j;
     float w4[4];
@@ -431,16 +433,16 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
     }
     *reinterpret_cast<float4*>(buf + 4 * j) = make_float4(w4[0], w4[1], w4[2], w4[3]);
   };
-  for (int j = tid; j < (int)jlo && j < nch; j += kLpSlots) edge(j);
-  for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += kLpSlots) edge(j);
+  for (int j = tid; j < (int)jlo && j < nch; j += nth) edge(j);
+  for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += nth) edge(j);
   // DMA: lanes of one instruction are consecutive chunks
-  for (int j0 = (int)(jlo & ~63LL) + wv * 64; j0 < jhi; j0 += 64 * kLpWaves) {
+  for (int j0 = (int)(jlo & ~63LL) + wv * 64; j0 < jhi; j0 += 64 * nwv) {
     const int j = j0 + ln;
     if (j >= jlo && j < jhi) __builtin_amdgcn_global_load_lds(xs + P0 + 4LL * j, buf + 4 * j0, 16, 0, 0);
   }
 }
 
-template <int CMAX, int K>
+template <int CMAX, int K, int LW>
 __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, int it, const float (&tp)[(CMAX + 6) / 4 * 4],
                                            int phi, int sub, int A, int ctop0, bool valid) {
   constexpr int NC = (CMAX + 6) / 4;
@@ -497,8 +499,8 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
   }
   // The next item's DMAs (issued before this scan) are waited for here,
   // before the output stores: vmcnt also counts stores, so a drain after them
-  // would wait out their write latency too.
-  dma_drain();
+  // would wait out their write latency too.  (LW: the loader wave stages.)
+  if (!LW) dma_drain();
   float* ys = a.y + (long long)st * a.y_stride;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -507,22 +509,34 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
   }
 }
 
-template <int CMAX, int K>
-__global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
+// LW = 1: an eighth wave stages every item (and commits the state) while
+// the seven compute waves only scan: the DMA issue -- 3-4 k cycles of each
+// compute wave's item time -- leaves their instruction
+// streams; its registers come free with the 2-waves-per-SIMD allocation.
+template <int CMAX, int K, int LW>
+__global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   __shared__ __attribute__((aligned(16))) float bufA[kLpBuf];
   __shared__ __attribute__((aligned(16))) float bufB[kLpBuf];
   __shared__ float cbuf[kLpSlots];  // the new state, in flight during the compute
   constexpr int U = (CMAX + 6) / 4 * 4;
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+  const bool loader = LW && wv == kLpWaves;  // wave-uniform
   // items: contiguous range per workgroup
   const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
   const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
   const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
   if (i0 >= i1) return;
+  auto stage = [&](float* buf, int it) __attribute__((always_inline)) {
+    if (a.ablate == 1) return;
+    if (!LW)
+      lp_stage<CMAX>(a, buf, it, threadIdx.x, kLpSlots, wv, kLpWaves, ln);
+    else if (loader)
+      lp_stage<CMAX>(a, buf, it, ln, 64, 0, 1, ln);
+  };
   // the first item's DMA runs while this lane's item and taps are loaded
-  if (a.ablate != 1) lp_stage<CMAX>(a, bufA, i0, wv, ln);
-  const int code = a.lanes[threadIdx.x];
+  stage(bufA, i0);
+  const int code = loader ? -1 : a.lanes[threadIdx.x];
   const bool valid = code >= 0;
   const int phi = valid ? (code & 0xffff) : 0, sub = valid ? (code >> 16) : 0;
   const int q = (int)((long long)phi * a.down / a.up);
@@ -530,40 +544,45 @@ __global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
   const int p = (int)((long long)phi * a.down % a.up);
   float tp[U];
   const float* row = a.hs + ((long long)A * a.up + p) * U;
+  if (!loader) {
 #pragma unroll
-  for (int u = 0; u < U; u += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(row + u);
-    tp[u] = v.x;
-    tp[u + 1] = v.y;
-    tp[u + 2] = v.z;
-    tp[u + 3] = v.w;
+    for (int u = 0; u < U; u += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(row + u);
+      tp[u] = v.x;
+      tp[u + 1] = v.y;
+      tp[u + 2] = v.z;
+      tp[u + 3] = v.w;
+    }
   }
   for (int it = i0; it < i1; ++it) {
-    // (the previous item drained its DMAs before its output stores)
-    if (it == i0 || a.ablate == 2) dma_drain();
+    // (the previous item drained its DMAs before its output stores; the
+    // loader drains its own here)
+    if (it == i0 || a.ablate == 2 || loader) dma_drain();
     __syncthreads();  // item it's span has landed; the other buffer is free
     // the stream's first item is the only reader of its old state and its span
-    // is staged now: state <- last ns inputs of the block (src/filter.cpp:169),
-    // brought into LDS by DMA during the compute and stored after it
-    // (ns <= kLpSlots on this path)
+    // is staged now: state <- last ns inputs of the block (src/filter.cpp:169)
+    // (ns <= kLpSlots on this path).  LW: the loader copies it directly
+    // (its own edge loads read the old state, before this); else it is
+    // brought into LDS by DMA during the compute and stored after it.
     const bool commit = it % a.nbat == 0;
-    if (commit && (int)threadIdx.x < a.ns)
+    if (LW) {
+      if (loader && commit) {
+        const long long s = it / a.nbat;
+        for (int j = ln; j < a.ns; j += 64) a.state[s * a.ns + j] = a.x[s * a.x_stride + (a.n - a.ns) + j];
+      }
+    } else if (commit && (int)threadIdx.x < a.ns) {
       __builtin_amdgcn_global_load_lds(a.x + (long long)(it / a.nbat) * a.x_stride + (a.n - a.ns) + threadIdx.x,
                                        cbuf + wv * 64, 4, 0, 0);
+    }
     const bool odd = ((it - i0) & 1) != 0;
-    if (it + 1 < i1 && a.ablate != 1) {
+    if (it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
+    if (a.ablate != 2 && !loader) {
       if (odd)
-        lp_stage<CMAX>(a, bufA, it + 1, wv, ln);
+        lp_compute<CMAX, K, LW>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
       else
-        lp_stage<CMAX>(a, bufB, it + 1, wv, ln);
+        lp_compute<CMAX, K, LW>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
     }
-    if (a.ablate != 2) {
-      if (odd)
-        lp_compute<CMAX, K>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
-      else
-        lp_compute<CMAX, K>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
-    }
-    if (commit && (int)threadIdx.x < a.ns) {
+    if (!LW && commit && (int)threadIdx.x < a.ns) {
       dma_drain();
       a.state[(long long)(it / a.nbat) * a.ns + threadIdx.x] = cbuf[threadIdx.x];
     }
@@ -573,6 +592,12 @@ __global__ __launch_bounds__(kLpSlots, 1) void resample_lp(LpArgs a) {
 // read per launch (a getenv scan), so a test can switch kernels in-process
 bool lp_enabled() {
   const char* e = std::getenv("SDR_RESAMPLE_LP");
+  return !e || std::atoi(e) != 0;
+}
+
+// read per launch (a getenv scan), so a test can switch kernels in-process
+bool lp_loader() {
+  const char* e = std::getenv("SDR_RESAMPLE_LOADER");
   return !e || std::atoi(e) != 0;
 }
 
@@ -669,16 +694,33 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
         if ((*err = hipGetLastError()) != hipSuccess) return true;
       }
       const int grid = b.nitems < ncu ? b.nitems : ncu;
-      if (cmax == 151) {
-        if (K == 4)
-          hipLaunchKernelGGL((resample_lp<151, 4>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
-        else
-          hipLaunchKernelGGL((resample_lp<151, 7>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
+      const dim3 g((unsigned)grid);
+      if (lp_loader()) {
+        const dim3 blk(kLpSlots + 64);
+        if (cmax == 151) {
+          if (K == 4)
+            hipLaunchKernelGGL((resample_lp<151, 4, 1>), g, blk, 0, st, b);
+          else
+            hipLaunchKernelGGL((resample_lp<151, 7, 1>), g, blk, 0, st, b);
+        } else {
+          if (K == 4)
+            hipLaunchKernelGGL((resample_lp<101, 4, 1>), g, blk, 0, st, b);
+          else
+            hipLaunchKernelGGL((resample_lp<101, 7, 1>), g, blk, 0, st, b);
+        }
       } else {
-        if (K == 4)
-          hipLaunchKernelGGL((resample_lp<101, 4>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
-        else
-          hipLaunchKernelGGL((resample_lp<101, 7>), dim3((unsigned)grid), dim3(kLpSlots), 0, st, b);
+        const dim3 blk(kLpSlots);
+        if (cmax == 151) {
+          if (K == 4)
+            hipLaunchKernelGGL((resample_lp<151, 4, 0>), g, blk, 0, st, b);
+          else
+            hipLaunchKernelGGL((resample_lp<151, 7, 0>), g, blk, 0, st, b);
+        } else {
+          if (K == 4)
+            hipLaunchKernelGGL((resample_lp<101, 4, 0>), g, blk, 0, st, b);
+          else
+            hipLaunchKernelGGL((resample_lp<101, 7, 0>), g, blk, 0, st, b);
+        }
       }
       *err = hipGetLastError();
       *state_done = true;  // resample_lp commits the state itself

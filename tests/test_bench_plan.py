@@ -159,3 +159,24 @@ def test_torchrun_ranks_use_gloo_and_max_time():
     assert line["ms_per_step"] == pytest.approx(0.3)  # max(2, 3) ms / 10 steps
     assert line["per_gpu"]["ms_per_step"] == [pytest.approx(0.2), pytest.approx(0.3)]
     assert "gloo" in line["config"]["parallelism"]
+
+
+def test_roofline_picks_the_binding_roof():
+    """cfg2 (8.4 B, 41.3 FLOP per pair) is HBM-bound; the u8 wire format (2.4 B) and
+    the resampler (4.735 B, 55.5 FLOP per input) sit above the exact-arithmetic ridge
+    (one FLOP per lane per VALU issue: 78.65 TFLOP/s), so their line reports VALU."""
+    b = _bench()
+    base = {"metric": "m", "tolerance": None, "bound": "hbm"}
+    cfg2 = dict(base, units=1024 * 65540, bytes_per_pair=8.4, flops_per_unit=41.3, kind="frontend_f32")
+    r = b.roofline(cfg2, 0.1, "none")
+    assert r["bound"] == "hbm" and r["frac"] == r["hbm_frac"]
+    assert r["frac"] == pytest.approx(1024 * 65540 * 8.4 / 1e-4 / 1e9 / 8000, abs=1e-4)
+    u8 = dict(cfg2, bytes_per_pair=2.4, kind="frontend_u8")
+    r = b.roofline(u8, 0.08, "none")
+    assert r["bound"] == "valu" and r["valu_peak_tflops"] == pytest.approx(157.3 / 2)
+    assert b.roofline(u8, 0.08, "none", "fma")["valu_peak_tflops"] == pytest.approx(157.3)
+    cfg3 = dict(base, units=1024 * 65600, bytes_per_pair=4.0 + 4.0 * 147 / 800,
+                flops_per_unit=2.0 * 151 * 147 / 800, kind="resample")
+    r = b.roofline(cfg3, 0.136, "none")
+    assert r["bound"] == "valu" and r["frac"] == r["valu_frac"]
+    assert r["hbm_frac"] == pytest.approx(0.29, abs=0.01)

@@ -152,9 +152,14 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
 RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
                   (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                   (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
-# resample_lp (default), then resample_rs, then the phase-major resample_pp
-RESAMPLE_KERNELS = {"lp": {}, "rs": {"SDR_RESAMPLE_LP": "0"},
-                    "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
+# resample_sg (experimental, off by default), resample_lp without and with its
+# loader wave (the default), then
+# resample_rs, then the phase-major resample_pp
+RESAMPLE_KERNELS = {"sg": {"SDR_RESAMPLE_SG": "1"},
+                    "lp": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LOADER": "0"},
+                    "lpw": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LOADER": "1"},
+                    "rs": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LP": "0"},
+                    "pp": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
 
 
 @pytest.mark.parametrize("kernel", list(RESAMPLE_KERNELS))
@@ -188,6 +193,42 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
         for s in range(nstreams):
             assert_bits(got[s], oracle.resample(up, down, x[s], h, states[s]), f"stream {s} block {blk}")
         assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
+
+
+@pytest.mark.parametrize("kernel", ["sg", "lpw", "lp"])
+@pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 8000), (147, 1280, 101, 100, 12800)])
+def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
+    """Inf and NaN inputs (and in the carried state): every output equals the
+    reference's -- bitwise where it is a number or an infinity, NaN where the
+    reference's is NaN.  resample_sg pads each phase pair's windows with zero
+    taps; a staged Inf/NaN switches its unit to the masked scan, so a padding
+    product never turns an output NaN that the reference keeps finite."""
+    for k, v in RESAMPLE_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
+    sdrhip = built_lib
+    nstreams = 3
+    rng = np.random.default_rng(7 + up)
+    h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
+    ny = sdrhip.resample_out_len(up, down, n)
+    states = [rng.standard_normal(ns).astype(np.float32) for _ in range(nstreams)]
+    states[1][ns // 2] = np.inf
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_st = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.stack(states))
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * ny * 4)
+    x = rng.standard_normal((nstreams, n)).astype(np.float32)
+    x[0, 1000] = np.nan
+    x[0, 3001] = -np.inf
+    x[2, n - 300] = np.inf
+    d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+    gpu_ctx.resample_dev(up, down, d_x, n, nstreams, n, d_h, len(h), d_st, ns, d_y, ny)
+    gpu_ctx.synchronize()
+    got = d_y.download().reshape(nstreams, ny)
+    for s in range(nstreams):
+        ref = np.asarray(oracle.resample(up, down, x[s], h, states[s]), dtype=np.float32)
+        nan = np.isnan(ref)
+        assert np.array_equal(np.isnan(got[s]), nan), f"stream {s}: NaN positions differ"
+        assert_bits(got[s][~nan], ref[~nan], f"stream {s}")
+        assert (~np.isfinite(ref)).any()  # the Inf / NaN reached some outputs
 
 
 @pytest.mark.parametrize("up,down,cnt,nstreams,n", [(147, 800, 151, 130, 8000), (147, 800, 101, 64, 4000),
