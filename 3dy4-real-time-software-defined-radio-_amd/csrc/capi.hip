@@ -594,16 +594,16 @@ int sdr_frontend_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
 
 static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                        const float* lp_tables, const float* sg_tables);
+                        const float* lp_tables);
 
 int sdr_resample_f32_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                          const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
-  return resample_dev(c, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, nullptr, nullptr);
+  return resample_dev(c, up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, nullptr);
 }
 
 static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                        const float* lp_tables, const float* sg_tables) {
+                        const float* lp_tables) {
   int rc = enter(c);
   if (rc) return rc;
   if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
@@ -625,7 +625,7 @@ static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long 
   float* hp = static_cast<float*>(scratch(c, kTmp, sdr::resample_scratch_floats(up, ntaps) * sizeof(float)));
   if (!hp) return scratch_fail(c, "polyphase table");
   hipError_t e = sdr::launch_resample(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, hp,
-                                      c->cur, lp_tables, sg_tables);
+                                      c->cur, lp_tables);
   if (e != hipSuccess) return hip_fail(c, e, "resample launch");
   return SDR_OK;
 }
@@ -634,7 +634,6 @@ struct sdr_resample_plan {
   int up = 0, down = 0, ntaps = 0;
   const float* h = nullptr;
   float* tables = nullptr;  // resample_lp's tables, or nullptr when the shape takes another kernel
-  float* sg = nullptr;      // resample_sg's tables, or nullptr
 };
 
 int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int ntaps, sdr_resample_plan** out) {
@@ -648,25 +647,10 @@ int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int n
   p->down = down;
   p->ntaps = ntaps;
   p->h = h;
-  if (up > 1 && sdr::resample_sg_covers(up, down, ntaps, ntaps / up - 1)) {
-    const size_t bytes = sdr::resample_sg_table_floats(up, ntaps) * sizeof(float);
-    hipError_t e = hipMalloc(&p->sg, bytes);
-    if (e != hipSuccess) {
-      delete p;
-      return fail(c, SDR_ENOMEM, "resample plan tables");
-    }
-    if (!sdr::resample_sg_tables(up, down, h, ntaps, p->sg, c->cur, &e) || e != hipSuccess ||
-        (e = hipStreamSynchronize(c->cur)) != hipSuccess) {
-      (void)hipFree(p->sg);
-      delete p;
-      return hip_fail(c, e == hipSuccess ? hipErrorInvalidValue : e, "resample plan tables");
-    }
-  }
   if (up > 1) {
     const size_t bytes = sdr::resample_rs_scratch_floats(up, ntaps) * sizeof(float);
     hipError_t e = hipMalloc(&p->tables, bytes);
     if (e != hipSuccess) {
-      if (p->sg) (void)hipFree(p->sg);
       delete p;
       return fail(c, SDR_ENOMEM, "resample plan tables");
     }
@@ -675,14 +659,12 @@ int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int n
       p->tables = nullptr;  // another kernel: built per call as before
     } else if (e != hipSuccess) {
       (void)hipFree(p->tables);
-      if (p->sg) (void)hipFree(p->sg);
       delete p;
       return hip_fail(c, e, "resample plan tables");
     } else if ((e = hipStreamSynchronize(c->cur)) != hipSuccess) {
       // built before the plan is handed out: a later call may run on
       // another stream (sdr_ctx_set_stream), which nothing would order
       (void)hipFree(p->tables);
-      if (p->sg) (void)hipFree(p->sg);
       delete p;
       return hip_fail(c, e, "resample plan tables");
     }
@@ -695,11 +677,10 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
   int rc = enter(c);
   if (rc) return rc;
   if (p) {
-    if (p->tables || p->sg) {
+    if (p->tables) {
       // every stream that used the plan, not only the current one
       (void)hipDeviceSynchronize();
-      if (p->tables) (void)hipFree(p->tables);
-      if (p->sg) (void)hipFree(p->sg);
+      (void)hipFree(p->tables);
     }
     delete p;
   }
@@ -709,8 +690,7 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
 int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const float* x, long long n, int nstreams,
                               long long x_stride, float* state, int ns, float* y, long long y_stride) {
   if (!p) return fail(c, SDR_EINVAL, "null plan");
-  return resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->tables,
-                      p->sg);
+  return resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->tables);
 }
 
 int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,

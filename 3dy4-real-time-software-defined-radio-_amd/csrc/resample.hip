@@ -326,21 +326,12 @@ size_t resample_scratch_floats(int up, int ntaps) {
   const int cmax = (ntaps + up - 1) / up;
   const size_t pp = (size_t)up * (size_t)((cmax + 3) / 4 * 4);
   const size_t rs = resample_rs_scratch_floats(up, ntaps);
-  const size_t sg = resample_sg_table_floats(up, ntaps);
-  return std::max(std::max(pp, rs), sg);
+  return std::max(pp, rs);
 }
 
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables,
-                           const float* sg_tables) {
-  {
-    // resample_sg.hip first (column lanes, SGPR taps, phase pairs)
-    hipError_t e = hipSuccess;
-    if (launch_resample_sg(up, down, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, ny, scratch_taps,
-                           sg_tables, st, &e))
-      return e;
-  }
+                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables) {
   {
     // resample_rs.hip's kernels first (lane-phase, then sliding-window), for the shapes they cover
     hipError_t e = hipSuccess;

@@ -76,11 +76,9 @@ hipError_t launch_demod(const float* I, const float* Q, long long n, int nstream
                         float* prev_i, float* prev_q, float* out, long long out_stride, hipStream_t st);
 // lp_tables: resample_lp's tables prebuilt by resample_lp_tables (a plan),
 // or nullptr to build them into scratch_taps for this call
-// sg_tables: resample_sg's, prebuilt by resample_sg_tables (a plan), or nullptr
 hipError_t launch_resample(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
                            const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
-                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables = nullptr,
-                           const float* sg_tables = nullptr);
+                           long long ny, float* scratch_taps, hipStream_t st, const float* lp_tables = nullptr);
 hipError_t launch_delay(const float* in, long long n, int nstreams, long long in_stride, float* state, int ns,
                         float* out, long long out_stride, hipStream_t st);
 hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
@@ -145,17 +143,5 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
 // resample_lp covers.
 bool resample_lp_tables(int up, int down, const float* h, int ntaps, int ns, float* tables, hipStream_t st,
                         hipError_t* err);
-// Column-lane resampler with SGPR taps and phase pairs (resample_sg.hip), the
-// default for the shapes it covers: its table size (an upper bound over
-// down), whether it takes (up, down, ntaps, ns), its table build (false =
-// not covered) and its launch (false = not covered; tables nullptr = build
-// them into scratch for this call).  It commits the state itself.
-size_t resample_sg_table_floats(int up, int ntaps);
-bool resample_sg_covers(int up, int down, int ntaps, int ns);
-bool resample_sg_tables(int up, int down, const float* h, int ntaps, float* tables, hipStream_t st,
-                        hipError_t* err);
-bool launch_resample_sg(int up, int down, const float* x, long long n, int nstreams, long long x_stride,
-                        const float* h, int ntaps, float* state, int ns, float* y, long long y_stride, long long ny,
-                        float* scratch, const float* tables, hipStream_t st, hipError_t* err);
 
 }  // namespace sdr

@@ -152,14 +152,11 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
 RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
                   (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                   (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
-# resample_sg (experimental, off by default), resample_lp without and with its
-# loader wave (the default), then
-# resample_rs, then the phase-major resample_pp
-RESAMPLE_KERNELS = {"sg": {"SDR_RESAMPLE_SG": "1"},
-                    "lp": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LOADER": "0"},
-                    "lpw": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LOADER": "1"},
-                    "rs": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LP": "0"},
-                    "pp": {"SDR_RESAMPLE_SG": "0", "SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
+# resample_lp with its loader wave (the default) and without, then resample_rs,
+# then the phase-major resample_pp
+RESAMPLE_KERNELS = {"lpw": {"SDR_RESAMPLE_LOADER": "1"}, "lp": {"SDR_RESAMPLE_LOADER": "0"},
+                    "rs": {"SDR_RESAMPLE_LP": "0"},
+                    "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
 
 
 @pytest.mark.parametrize("kernel", list(RESAMPLE_KERNELS))
@@ -195,14 +192,13 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
         assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
 
 
-@pytest.mark.parametrize("kernel", ["sg", "lpw", "lp"])
+@pytest.mark.parametrize("kernel", ["lpw", "lp", "rs"])
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 8000), (147, 1280, 101, 100, 12800)])
 def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
     """Inf and NaN inputs (and in the carried state): every output equals the
     reference's -- bitwise where it is a number or an infinity, NaN where the
-    reference's is NaN.  resample_sg pads each phase pair's windows with zero
-    taps; a staged Inf/NaN switches its unit to the masked scan, so a padding
-    product never turns an output NaN that the reference keeps finite."""
+    reference's is NaN.  resample_lp and resample_rs pad the window ends with
+    zero taps and zeroed inputs (term +0), never 0 * Inf."""
     for k, v in RESAMPLE_KERNELS[kernel].items():
         monkeypatch.setenv(k, v)
     sdrhip = built_lib
