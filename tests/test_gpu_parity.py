@@ -113,7 +113,8 @@ def test_fir_decim_vs_oracle(gpu_ctx, oracle, D, ntaps, ns, n):
 
 
 @pytest.mark.parametrize("D,n,ns", [(10, 5130, 100), (10, 5130, 150), (10, 2000, 200), (5, 4105, 100),
-                                    (5, 4105, 128), (10, 110, 100), (10, 200, 180)])
+                                    (5, 4105, 128), (10, 110, 100), (10, 200, 180), (10, 130, 120),
+                                    (10, 65530, 100), (10, 65550, 300)])
 def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, D, n, ns):
     """Fused front end (f32 and u8 wire) where the tiled kernel's edge
     handling matters: n % 4 != 0 (a chunk straddles the block end), state
