@@ -29,8 +29,8 @@ struct sdr_ctx {
   // (sdr_ctx_set_stereo_fork; SDR_STEREO_FORK sets the default at creation)
   int stereo_fork = -1;
   // grow-only device scratch for the host-pointer wrappers and internal use
-  void* buf[19] = {};
-  size_t cap[19] = {};
+  void* buf[20] = {};
+  size_t cap[20] = {};
   // live graphs recorded on this context: they hold pointers into buf[], so
   // scratch() refuses to reallocate while any exists (or while capturing)
   int graphs = 0;
@@ -42,7 +42,7 @@ namespace {
 
 enum Slot {
   kX0 = 0, kX1, kH, kS0, kS1, kY0, kY1, kOut, kPrev, kTmp,
-  kPipe0, kPipe1, kPipe2, kPipe3, kPipe4, kPipe5, kPipe6, kPipe7, kPipe8
+  kPipe0, kPipe1, kPipe2, kPipe3, kPipe4, kPipe5, kPipe6, kPipe7, kPipe8, kGuard
 };
 
 int fail(sdr_ctx* c, int code, const char* fmt, ...) {
@@ -787,8 +787,10 @@ int sdr_fm_pll_dev(sdr_ctx* c, const float* in, long long n, int nstreams, long 
   const long long astride = (n + 1 + 3) / 4 * 4;  // trigArg per sample (+ the incoming nco_state)
   float* args = static_cast<float*>(scratch(c, kPipe6, (size_t)nstreams * astride * sizeof(float)));
   if (!args) return scratch_fail(c, "pll argument buffer");
+  auto* guard = static_cast<uint8_t*>(scratch(c, kGuard, sdr::pll_guard_bytes(n, nstreams)));
+  if (!guard) return scratch_fail(c, "pll guard buffer");
   hipError_t e = sdr::launch_pll(in, n, nstreams, in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, mix,
-                                 mix_stride, out, out_stride, args, astride, c->cur);
+                                 mix_stride, out, out_stride, args, astride, c->cur, guard);
   if (e != hipSuccess) return hip_fail(c, e, "pll launch");
   return SDR_OK;
 }
@@ -828,7 +830,8 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
   float* slp = static_cast<float*>(scratch(c, kPipe5, abytes));
   float* args = static_cast<float*>(scratch(c, kPipe6, (size_t)nstreams * pstride * sizeof(float)));
   float* mixed = static_cast<float*>(scratch(c, kPipe7, dbytes));
-  if (!demod || !delayed || !mono || !pilot || !sband || !slp || !args || !mixed)
+  auto* guard = static_cast<uint8_t*>(scratch(c, kGuard, sdr::pll_guard_bytes(nd, nstreams)));
+  if (!demod || !delayed || !mono || !pilot || !sband || !slp || !args || !mixed || !guard)
     return scratch_fail(c, "pipeline buffers");
   if (!c->side) {
     SDR_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
@@ -885,7 +888,7 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
                                   st->ns_bpf, pilot, dstride)))
     return rc;
   hipError_t e = sdr::launch_pll_recurrence(pilot, nd, nstreams, dstride, 19e3f, audio_fs, 2.0f, 0.0f, 0.01f, st->pll,
-                                            args, pstride, c->cur);
+                                            args, pstride, c->cur, guard);
   if (e != hipSuccess) return hip_fail(c, e, "pll launch");
   // join: the NCO mixed with the stereo band (pointwiseMultiply x2, :127)
   if (fork) SDR_HIP(c, hipStreamWaitEvent(c->cur, c->join, 0));

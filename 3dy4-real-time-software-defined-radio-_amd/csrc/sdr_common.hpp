@@ -84,16 +84,20 @@ hipError_t launch_delay(const float* in, long long n, int nstreams, long long in
 hipError_t launch_pcm(const float* x, long long n, int nstreams, long long x_stride, int16_t* pcm,
                       long long pcm_stride, hipStream_t st);
 // Stereo back end (stereo.hip): fmPLL one lane per stream, optionally fused
-// with the x2 mixer; L/R + interleave + s16 output stage.
+// with the x2 mixer; L/R + interleave + s16 output stage.  guard: scratch of
+// pll_guard_bytes(n, nstreams) for the certified step's per-chunk input
+// checks (computed in parallel before the recurrence), or nullptr to check
+// inside the recurrence.
+size_t pll_guard_bytes(long long n, int nstreams);
 hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
                       float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
                       long long mix_stride, float* out, long long out_stride, float* args, long long args_stride,
-                      hipStream_t st);
+                      hipStream_t st, uint8_t* guard);
 // the two halves of launch_pll: the per-stream recurrence (records each
 // sample's oscillator argument in args) and the parallel NCO (+ mixer)
 hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
                                  float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
-                                 long long args_stride, hipStream_t st);
+                                 long long args_stride, hipStream_t st, uint8_t* guard);
 hipError_t launch_nco(const float* args, long long args_stride, long long n, int nstreams, float nco_scale,
                       float phase_adjust, const float* mix, long long mix_stride, float* out, long long out_stride,
                       hipStream_t st);

@@ -41,11 +41,20 @@ constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
 // the recurrence's chain).  The stored arguments of the first pass are
 // rewritten by the second, so every output is the library path's or a
 // certified equal.
-template <int FAST>
+//
+// GUARD: where a chunk's input check (pllfast::input_ok on its 8 samples)
+// comes from -- 0: evaluated in the kernel, 1: guard[s * nchunk + c], written
+// by pll_guard_kernel over every stream and chunk in parallel beforehand.  The
+// check is off the recurrence's dependency chain, but the one wave per SIMD
+// issues every instruction itself: in the kernel it cost 7.6 % of stereo0
+// (profiles/r03_ab/pll_guard.txt).
+constexpr int kPllChunk = 8;
+template <int FAST, int GUARD>
 __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, long long n, int nstreams,
                                                  long long in_stride, float freq, float Fs, float nco_scale,
                                                  float phase_adjust, float norm_bw, float* __restrict__ pll,
-                                                 float* __restrict__ args, long long args_stride) {
+                                                 float* __restrict__ args, long long args_stride,
+                                                 const uint8_t* __restrict__ guard, long long nchunk) {
   const int s = blockIdx.x * 64 + threadIdx.x;
   if (s >= nstreams) return;
   const float* x = in + (long long)s * in_stride;
@@ -104,24 +113,29 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   // chunk ahead into registers, so no step waits on memory: a per-sample
   // load put a full load latency -- and the previous step's store, which
   // shares the vmcnt counter -- into every step.
-  constexpr int CH = 8;
+  constexpr int CH = kPllChunk;
   const long long nc = n / CH * CH;
   float xa[CH], xb[CH];
-  auto load = [&](float (&buf)[CH], long long k) __attribute__((always_inline)) {
+  int ga = 1, gb = 1;  // GUARD 1: the chunks' input checks
+  const uint8_t* gs = GUARD ? guard + (long long)s * nchunk : nullptr;
+  auto load = [&](float (&buf)[CH], int& g, long long k) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) buf[j] = x[k + j];
+    if constexpr (GUARD) g = gs[k / CH];
     // keep the loads here: left to the scheduler they sink to their use
     __builtin_amdgcn_sched_barrier(0);
   };
   // first: the kernel's first chunk, whose step 1 has no oscillator to rotate
   // from (the carried state holds only its floats) and runs the polynomial
-  auto run = [&](const float (&buf)[CH], long long k0, auto first) __attribute__((always_inline)) {
+  auto run = [&](const float (&buf)[CH], int g, long long k0, auto first) __attribute__((always_inline)) {
     if constexpr (FAST) {
       const float s0 = fbI, s1 = fbQ, s2 = integrator, s3 = phaseEst, s4 = trigOffset;
       // the chunk's inputs (already in registers, off the recurrence's chain)
-      int in_ok = 1;
+      int in_ok = g;
+      if constexpr (!GUARD) {
 #pragma unroll
-      for (int j = 0; j < CH; ++j) in_ok &= (int)pllfast::input_ok(buf[j]);
+        for (int j = 0; j < CH; ++j) in_ok &= (int)pllfast::input_ok(buf[j]);
+      }
       score = (start_ok && in_ok) ? ~0u : 0u;
       // unconditional: args rows hold n + 1 floats (launch_pll_recurrence), so
       // ar[n] is the row's spare slot -- no per-step bounds compare and branch
@@ -161,16 +175,16 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   // ping-pong register chunks (no copies, so no wait at the chunk boundary
   // beyond the chunk being consumed); a chunk past nc re-loads an in-bounds one
   if (nc > 0) {
-    load(xa, 0);
-    load(xb, CH < nc ? CH : 0);
-    run(xa, 0, std::true_type{});
+    load(xa, ga, 0);
+    load(xb, gb, CH < nc ? CH : 0);
+    run(xa, ga, 0, std::true_type{});
   }
   for (long long k0 = CH; k0 < nc; k0 += 2 * CH) {
-    load(xa, k0 + CH < nc ? k0 + CH : k0);
-    run(xb, k0, std::false_type{});
+    load(xa, ga, k0 + CH < nc ? k0 + CH : k0);
+    run(xb, gb, k0, std::false_type{});
     if (k0 + CH < nc) {
-      load(xb, k0 + 2 * CH < nc ? k0 + 2 * CH : k0);
-      run(xa, k0 + CH, std::false_type{});
+      load(xb, gb, k0 + 2 * CH < nc ? k0 + 2 * CH : k0);
+      run(xa, ga, k0 + CH, std::false_type{});
     }
   }
   for (long long k = nc; k < n; ++k) {  // ragged tail
@@ -183,6 +197,21 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   st[3] = phaseEst;
   st[4] = trigOffset;
   st[5] = (float)cos((double)(arg * nco_scale + phase_adjust));  // nco_state (:221-222)
+}
+
+// guard[s * nchunk + c] = 1 when every sample of the PLL's chunk c of stream
+// s passes pllfast::input_ok (0 or 2^-60 <= |v| <= FLT_MAX): the chunk guard
+// of the certified step, for all streams and chunks at once.
+__global__ __launch_bounds__(kWG) void pll_guard_kernel(const float* __restrict__ in, int nstreams, long long in_stride,
+                                                        uint8_t* __restrict__ guard, long long nchunk) {
+  const int s = blockIdx.y;
+  const long long c = (long long)blockIdx.x * kWG + threadIdx.x;
+  if (c >= nchunk) return;
+  const float* x = in + (long long)s * in_stride + c * kPllChunk;
+  int ok = 1;
+#pragma unroll
+  for (int j = 0; j < kPllChunk; ++j) ok &= (int)pllfast::input_ok(x[j]);
+  guard[(long long)s * nchunk + c] = (uint8_t)ok;
 }
 
 // ncoOut[k] from the recorded arguments (k = 0: the old nco_state), optionally
@@ -217,21 +246,39 @@ __global__ __launch_bounds__(kWG) void stereo_pcm_kernel(const float* __restrict
 
 // args: [nstreams][args_stride] with args_stride >= n + 1 (args[s][n] is
 // written, a spare slot: the kernel stores every step's argument unguarded)
+size_t pll_guard_bytes(long long n, int nstreams) {
+  const long long nchunk = n / kPllChunk;
+  return (size_t)(nchunk > 0 ? nchunk : 1) * (size_t)(nstreams > 0 ? nstreams : 1);
+}
+
 hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
                                  float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
-                                 long long args_stride, hipStream_t st) {
+                                 long long args_stride, hipStream_t st, uint8_t* guard) {
   if (args_stride < n + 1) return hipErrorInvalidValue;
-  // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests)
+  const dim3 grid((unsigned)((nstreams + 63) / 64)), block(64);
+  const long long nchunk = n / kPllChunk;
+  // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests);
+  // SDR_PLL_GUARD=0 evaluates the input check inside the recurrence (A/B)
   const int fast = env_int("SDR_PLL_FAST", 1);
+  const bool pre = guard && nchunk > 0 && env_int("SDR_PLL_GUARD", 1) != 0;
+  if (fast && pre) {
+    hipLaunchKernelGGL(pll_guard_kernel, dim3((unsigned)((nchunk + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0,
+                       st, in, nstreams, in_stride, guard, nchunk);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   if (fast == 2)
-    hipLaunchKernelGGL(pll_kernel<2>, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams,
-                       in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+    hipLaunchKernelGGL((pll_kernel<2, 0>), grid, block, 0, st, in, n, nstreams, in_stride, freq, Fs, nco_scale,
+                       phase_adjust, norm_bw, pll, args, args_stride, nullptr, 0LL);
+  else if (fast && pre)
+    hipLaunchKernelGGL((pll_kernel<1, 1>), grid, block, 0, st, in, n, nstreams, in_stride, freq, Fs, nco_scale,
+                       phase_adjust, norm_bw, pll, args, args_stride, guard, nchunk);
   else if (fast)
-    hipLaunchKernelGGL(pll_kernel<1>, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams,
-                       in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+    hipLaunchKernelGGL((pll_kernel<1, 0>), grid, block, 0, st, in, n, nstreams, in_stride, freq, Fs, nco_scale,
+                       phase_adjust, norm_bw, pll, args, args_stride, nullptr, 0LL);
   else
-    hipLaunchKernelGGL(pll_kernel<0>, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, st, in, n, nstreams,
-                       in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll, args, args_stride);
+    hipLaunchKernelGGL((pll_kernel<0, 0>), grid, block, 0, st, in, n, nstreams, in_stride, freq, Fs, nco_scale,
+                       phase_adjust, norm_bw, pll, args, args_stride, nullptr, 0LL);
   return hipGetLastError();
 }
 
@@ -246,9 +293,9 @@ hipError_t launch_nco(const float* args, long long args_stride, long long n, int
 hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_stride, float freq, float Fs,
                       float nco_scale, float phase_adjust, float norm_bw, float* pll, const float* mix,
                       long long mix_stride, float* out, long long out_stride, float* args, long long args_stride,
-                      hipStream_t st) {
+                      hipStream_t st, uint8_t* guard) {
   hipError_t e = launch_pll_recurrence(in, n, nstreams, in_stride, freq, Fs, nco_scale, phase_adjust, norm_bw, pll,
-                                       args, args_stride, st);
+                                       args, args_stride, st, guard);
   if (e != hipSuccess) return e;
   return launch_nco(args, args_stride, n, nstreams, nco_scale, phase_adjust, mix, mix_stride, out, out_stride, st);
 }

@@ -589,15 +589,19 @@ def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
         assert_bits(res["1"][1][s], ost, f"stream {s} state vs oracle")
 
 
-def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch):
+@pytest.mark.parametrize("guard,n", [("1", 4096), ("0", 4096), ("1", 4093)])
+def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch, guard, n):
     """The certified path (its rotation phase detector, the 1,024-ulp window
     and the chunk guards) on inputs far from a pilot: magnitudes 2^-40..2^40
     with random signs, 2 % exact zeros, 1 % tiny or subnormal samples
     (2^-149..2^-60), constant and all-zero streams; every
-    result bitwise equal to the library path, 4 streams to the oracle."""
+    result bitwise equal to the library path, 4 streams to the oracle.
+    guard: the chunks' input checks from the parallel pre-pass (1, default)
+    or inside the recurrence (SDR_PLL_GUARD=0); n = 4093 leaves a ragged tail."""
     sdrhip = built_lib
+    monkeypatch.setenv("SDR_PLL_GUARD", guard)
     rng = np.random.default_rng(11)
-    S, n, Fs = 256, 4096, 240e3
+    S, Fs = 256, 240e3
     x = (rng.choice([-1.0, 1.0], (S, n)) * np.exp2(rng.uniform(-40, 40, (S, n)))).astype(np.float32)
     x[rng.uniform(size=(S, n)) < 0.02] = 0.0
     # tiny and subnormal samples (2^-149 .. 2^-60): outside pllfast::input_ok,
