@@ -99,9 +99,11 @@ __device__ __forceinline__ uint2 ldg_stream(const uint2* p) {
 // library.  Per workgroup, 8 words: HW_ID | XCC_ID << 32, s_memrealtime at
 // entry, then s_memtime sums over the workgroup's tiles of: the wait for a
 // tile's loads (top of the tile -> landed), staging, scan, epilogue; the
-// tile count; s_memrealtime at the end.
+// tile count; s_memrealtime at the end; s_memtime at entry and at the end
+// (their ratio to the realtime span is the shader clock).
 constexpr int kTraceWG = 1 << 17;
-__device__ unsigned long long g_fir_trace[kTraceWG * 8];
+constexpr int kTraceW = 10;  // words per record
+__device__ unsigned long long g_fir_trace[kTraceWG * kTraceW];
 #endif
 
 namespace sdr {
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   }
   if (first >= last) return;
 #ifdef SDR_FIR_TRACE
-  unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime(), tr_m0 = __builtin_amdgcn_s_memtime();
 #define SDR_TRACE_AT(i)                                        \
   {                                                            \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
@@ -677,7 +679,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     ++tr_n;
   }
   if (tid == 0 && blockIdx.x < kTraceWG) {
-    unsigned long long* o = g_fir_trace + 8ull * blockIdx.x;
+    unsigned long long* o = g_fir_trace + (unsigned long long)kTraceW * blockIdx.x;
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
     o[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
@@ -686,6 +688,8 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     for (int i = 0; i < 4; ++i) o[2 + i] = tr_sum[i];
     o[6] = tr_n;
     o[7] = __builtin_amdgcn_s_memrealtime();
+    o[8] = tr_m0;
+    o[9] = __builtin_amdgcn_s_memtime();
   }
 #else
   for (int lin = first; lin < last; lin += step) tile(lin, sa0, sa1);
@@ -764,7 +768,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
   const int first = claim();
   if (first < 0) return;
 #ifdef SDR_FIR_TRACE
-  unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime(), tr_m0 = __builtin_amdgcn_s_memtime();
 #define SDR_TRACE_AT(i)                                        \
   {                                                            \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
@@ -1056,7 +1060,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
 #undef SDR_TRACE_TILE
 #ifdef SDR_FIR_TRACE
   if (tid == 0 && blockIdx.x * 16 + wv < kTraceWG) {  // one record per wave
-    unsigned long long* o = g_fir_trace + 8ull * (blockIdx.x * 16 + wv);
+    unsigned long long* o = g_fir_trace + (unsigned long long)kTraceW * (blockIdx.x * 16 + wv);
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
     o[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
@@ -1065,6 +1069,8 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     for (int i = 0; i < 4; ++i) o[2 + i] = tr_sum[i];
     o[6] = tr_n;
     o[7] = __builtin_amdgcn_s_memrealtime();
+    o[8] = tr_m0;
+    o[9] = __builtin_amdgcn_s_memtime();
   }
 #endif
 }

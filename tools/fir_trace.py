@@ -6,7 +6,7 @@ bench's cfg2 launch, from a diagnostic build:
     SDRHIP_LIB=$PWD/ab/trace.so SDR_FIR_IQ=0 python tools/fir_trace.py [--config cfg2]
 
 Each workgroup of the traced launch records (csrc/fir_tile.hip,
-SDR_FIR_TRACE) its hardware slot, s_memtime sums over its tiles of the wait
+SDR_FIR_TRACE) its hardware slot, the shader clock over its lifetime, s_memtime sums over its tiles of the wait
 for a tile's loads, the staging, the scan and the epilogue, its tile count,
 and s_memrealtime (100 MHz, chip-wide) at entry and end.  Printed: the phase
 durations per tile, and per CU the time-averaged number of resident
@@ -48,9 +48,9 @@ def main():
     job.launch(1)
     job.torch.cuda.synchronize()
     nwg = 1 << 17
-    buf = np.zeros(nwg * 8, np.uint64)
+    buf = np.zeros(nwg * 10, np.uint64)
     assert fn(buf.ctypes.data, buf.nbytes, 0) == 0
-    t = buf.reshape(nwg, 8)
+    t = buf.reshape(nwg, 10)
     t = t[t[:, 6] != 0]
     job.close()
     hw = (t[:, 0] & 0xFFFFFFFF).astype(np.int64)
@@ -67,6 +67,10 @@ def main():
     ph = {"load wait (tile top -> loads landed)": per[:, 0], "stage (-> LDS staged)": per[:, 1],
           "scan": per[:, 2], "epilogue (demod, stores, state)": per[:, 3], "per tile": per.sum(1),
           "workgroup lifetime (realtime us)": (r1 - r0) / 100.0}
+    # shader clock inside the kernel: s_memtime ticks per realtime tick (100 MHz)
+    m0, m1 = t[:, 8].astype(np.int64), t[:, 9].astype(np.int64)
+    ok = r1 > r0
+    clock_mhz = (m1 - m0)[ok] / (r1 - r0)[ok] * 100.0
     out = {"config": cfg, "env": {k: v for k, v in os.environ.items() if k.startswith("SDR_")},
            "workgroups": int(len(t)), "tiles": int(ntile.sum()), "cus_seen": int(len(np.unique(key))),
            "phases_shader_ticks_per_tile": {k: {"p10": round(float(np.percentile(v, 10)), 1),
@@ -74,6 +78,9 @@ def main():
                                                 "mean": round(float(v.mean()), 1),
                                                 "p90": round(float(np.percentile(v, 90)), 1)}
                                             for k, v in ph.items()}}
+    out["shader_clock_mhz"] = {"median": round(float(np.median(clock_mhz)), 1),
+                               "p10": round(float(np.percentile(clock_mhz, 10)), 1),
+                               "p90": round(float(np.percentile(clock_mhz, 90)), 1)}
     # realtime (10 ns ticks): the kernel window and per-CU residency
     t0, t1 = r0.min(), r1.max()
     span = t1 - t0
