@@ -589,216 +589,6 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   }
 }
 
-// resample_sp2: resample_lp with each phase's tap row split over two
-// adjacent lanes, so a lane holds half a row (80 of 156 taps at C = 151) and
-// a CU runs four waves per SIMD instead of two.  Lane 2p (half 0) sums taps
-// u = 0 .. 4*H0-1 of its columns from 0.0f; lane 2p+1 (half 1) continues
-// those very sums over u = 4*H0 .. U-1 -- every output still visits its taps
-// in ascending order, one rounding per product and per sum.  The halves are
-// pipelined one step apart: at step s half 0 runs work unit s and half 1
-// runs unit s-1, starting from the running sums half 0 handed over by a DPP
-// lane move at the end of step s-1; half 1 stores the finished outputs.  A
-// unit is K columns of one item (G units per item, the item's columns in
-// unit order); items are staged into two LDS buffers by two loader waves,
-// which refill a buffer once both halves are past it (G-1 steps before half
-// 0 needs it).  Padding terms (zero taps, zeroed inputs) add +0: exact.
-constexpr int kSpWaves = 14;             // compute waves (+ two loaders)
-constexpr int kSpLanes = 64 * kSpWaves;  // 896 lanes = 448 lane pairs
-template <int CMAX, int K, int kSpG>
-__global__ __launch_bounds__(kSpLanes + 128, 1) void resample_sp2(LpArgs a) {
-  __shared__ __attribute__((aligned(16))) float bufA[kLpBuf];
-  __shared__ __attribute__((aligned(16))) float bufB[kLpBuf];
-  constexpr int U = (CMAX + 6) / 4 * 4;  // shifted row length (156 / 108)
-  constexpr int NC = U / 4;              // chunks per row
-  constexpr int H0 = (NC + 1) / 2;       // chunks per half (the second half's last may be padding)
-  constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) const f4v lds4;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-  const bool loader = wv >= kSpWaves;  // wave-uniform
-  const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
-  const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
-  const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
-  if (i0 >= i1) return;
-  const int lw = wv - kSpWaves;  // loader index (0, 1)
-  auto stage = [&](int j) __attribute__((always_inline)) {
-    // item i0 + j into buffer j % 2; a stream's first item then commits the
-    // new state (its staging read the old one: register loads, in order)
-    const int it = i0 + j;
-    if (a.ablate != 1) lp_stage<CMAX>(a, (j & 1) ? bufB : bufA, it, ln + 64 * lw, 128, lw, 2, ln);
-    if (lw == 0 && it % a.nbat == 0) {
-      const long long s = it / a.nbat;
-      for (int q = ln; q < a.ns; q += 64) a.state[s * a.ns + q] = a.x[s * a.x_stride + (a.n - a.ns) + q];
-    }
-  };
-  const int nunits = (i1 - i0) * kSpG;
-  // Lane table (bank classes): a ds_read_b128 serves a wave in four groups
-  // of 16 lanes, and two lanes of a group conflict when their chunk indices
-  // agree mod 16.  A pair's half-1 lane reads H0 = 20 chunks below its
-  // half-0 lane (class - 4), so a group whose half-0 classes are
-  // {0..3, 8..11} (or {4..7, 12..15}) covers all 16 classes once.  Pair
-  // (phi, sub) has class (sub*M/4 + ctop0(phi)) mod 16 for every column of
-  // every unit (the column stride adds the same to every lane); each class's
-  // first 28 pairs go to the slots that want it, the rest to free slots.
-  __shared__ int sp_cnt[16], sp_nfree, sp_nov, sp_used[kSpLanes / 2], sp_free[kSpLanes / 2], sp_code[kSpLanes];
-  if (!loader) {
-    const int t = threadIdx.x;
-    const int npair = a.up * a.S;
-    if (t < 16) sp_cnt[t] = 0;
-    if (t == 0) sp_nfree = sp_nov = 0;
-    if (t < kSpLanes / 2) sp_used[t] = 0;
-    sp_code[t] = -1;
-  }
-  __syncthreads();
-  int cls = 0, rank = 0;
-  const int npair = a.up * a.S;
-  const int t = threadIdx.x;
-  auto slot_lane = [](int slot, int h) {  // pair slot -> lane: group (wave, quarter), member m
-    const int grp = slot >> 3, m = slot & 7;
-    return (grp >> 2) * 64 + kB128Groups[grp & 3][2 * m + h];
-  };
-  if (!loader && t < npair) {
-    const int phi = t % a.up, sub = t / a.up;
-    const int q = (int)((long long)phi * a.down / a.up);
-    cls = (sub * (a.down >> 2) + ((q - base0) >> 2)) & 15;
-    rank = atomicAdd(&sp_cnt[cls], 1);
-    if (rank < kSpLanes / 32) {
-      // groups alternate type: even groups want half-0 classes {0..3, 8..11}
-      const int grp = 2 * rank + ((cls >> 2) & 1);
-      const int m = (cls & 3) | ((cls >> 3) << 2);
-      sp_used[grp * 8 + m] = 1;
-      sp_code[slot_lane(grp * 8 + m, 0)] = t;
-      sp_code[slot_lane(grp * 8 + m, 1)] = t;
-    }
-  }
-  __syncthreads();
-  if (!loader && t < kSpLanes / 2 && !sp_used[t]) sp_free[atomicAdd(&sp_nfree, 1)] = t;
-  __syncthreads();
-  if (!loader && t < npair && rank >= kSpLanes / 32) {
-    const int slot = sp_free[atomicAdd(&sp_nov, 1)];
-    sp_code[slot_lane(slot, 0)] = t;
-    sp_code[slot_lane(slot, 1)] = t;
-  }
-  __syncthreads();
-  if (loader) {
-    stage(0);
-    if (i0 + 1 < i1) stage(1);
-    for (int s = 0; s <= nunits; ++s) {
-      // half 0 starts item s / G at step s: its span must have landed
-      if (s % kSpG == 0) dma_drain();
-      __syncthreads();
-      // after barrier s = (j+1)G + 1 half 1 has finished item j's last unit
-      // ((j+1)G - 1, run at step (j+1)G): refill its buffer with item j + 2
-      if (s > kSpG && (s - 1) % kSpG == 0) {
-        const int j = (s - 1) / kSpG - 1;
-        if (i0 + j + 2 < i1) stage(j + 2);
-      }
-    }
-    return;
-  }
-  const int code = sp_code[threadIdx.x], hf = (int)threadIdx.x & 1;
-  const bool valid = code >= 0;
-  const int pr = valid ? code : 0;
-  const int phi = valid ? pr % a.up : 0, sub = valid ? pr / a.up : 0;
-  const int q = (int)((long long)phi * a.down / a.up);
-  const int A = (q - base0) & 3, ctop0 = (q - base0) >> 2;
-  const int p = (int)((long long)phi * a.down % a.up);
-  // this half's taps: row u = 4*H0*hf + i (0 past the row)
-  float tp[4 * H0];
-  {
-    const float* row = a.hs + ((long long)A * a.up + p) * U + 4 * H0 * hf;
-#pragma unroll
-    for (int c = 0; c < H0; ++c) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (4 * H0 * hf + 4 * c < U) v = *reinterpret_cast<const float4*>(row + 4 * c);
-      tp[4 * c] = v.x;
-      tp[4 * c + 1] = v.y;
-      tp[4 * c + 2] = v.z;
-      tp[4 * c + 3] = v.w;
-    }
-  }
-  float carry[K];  // half 1: the running sums half 0 handed over
-#pragma unroll
-  for (int k = 0; k < K; ++k) carry[k] = 0.0f;
-  const int ccl = H0 * hf;  // this half's first chunk (u = 4*cc ..)
-  for (int s = 0; s <= nunits; ++s) {
-    __syncthreads();
-    const int u = s - hf;  // this half's work unit
-    const bool live = valid && u >= 0 && u < nunits;
-    const int uu = u < 0 ? 0 : (u >= nunits ? nunits - 1 : u);
-    const int j = uu / kSpG, g = uu - j * kSpG;
-    const int it = i0 + j;
-    const int st = it / a.nbat, b = it - st * a.nbat;
-    const int t0 = b * a.C;
-    const int ce = min(a.C, a.np - t0);
-    const float* buf = (j & 1) ? bufB : bufA;
-    lds4* ptr[K];
-    bool act[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int c = sub + a.S * (g * K + k);
-      act[k] = live && c < ce;
-      const int cc = c < ce ? c : 0;
-      // the half's lowest chunk: chunk ci of the half at ptr[k][H0 - 1 - ci]
-      ptr[k] = (lds4*)(buf + 4 * (cc * (a.down >> 2) + ctop0 - H0 * hf - (H0 - 1)));
-      asm volatile("" : "+v"(ptr[k]));
-    }
-    float acc[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = hf ? carry[k] : 0.0f;
-#pragma unroll
-    for (int ci = 0; ci < H0; ++ci) {
-      if (a.ablate == 2) break;  // timing experiments only
-      f4v cur[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) cur[k] = ptr[k][H0 - 1 - ci];
-      __builtin_amdgcn_sched_barrier(0);
-      // only the row's ends hold out-of-window elements (half 0's first chunk,
-      // half 1's last chunks, and its padding chunk past the row): there the
-      // shifted tap is 0 and the input is replaced by 0 (term +0)
-      constexpr bool kLo = true;
-#pragma unroll
-      for (int jj = 3; jj >= 0; --jj) {
-        const int ur0 = 4 * ci + 3 - jj, ur1 = 4 * (H0 + ci) + 3 - jj;  // row index u per half
-        bool ok = true;
-        if (ci == 0) ok = hf || ur0 + A - 3 >= 0;
-        if (4 * (H0 + ci) + 3 >= CMAX) ok = !hf || (ur1 < U && ur1 + A - 3 < CMAX);
-        (void)kLo;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float v = cur[k][jj];
-          if (ci == 0 || 4 * (H0 + ci) + 3 >= CMAX) v = ok ? v : 0.0f;
-          acc[k] = acc[k] + tp[4 * ci + 3 - jj] * v;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) asm volatile("" : "+v"(acc[k]));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // half 1 holds finished outputs; half 0 hands its sums to half 1
-    if (hf) {
-      float* ys = a.y + (long long)st * a.y_stride;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const long long jo = (long long)a.up * (t0 + sub + a.S * (g * K + k)) + phi;
-        if (act[k] && jo < a.ny) ys[jo] = acc[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      // quad_perm [0,0,2,2]: lane 2p+1 reads lane 2p
-      carry[k] = __int_as_float(
-          __builtin_amdgcn_update_dpp(0, __float_as_int(acc[k]), 0xA0, 0xF, 0xF, false));
-    }
-  }
-}
-
-// read per launch (a getenv scan), so a test can switch kernels in-process
-bool sp2_enabled() {
-  const char* e = std::getenv("SDR_RESAMPLE_SP2");
-  return e && std::atoi(e) != 0;
-}
-
 // read per launch (a getenv scan), so a test can switch kernels in-process
 bool lp_enabled() {
   const char* e = std::getenv("SDR_RESAMPLE_LP");
@@ -905,26 +695,6 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       }
       const int grid = b.nitems < ncu ? b.nitems : ncu;
       const dim3 g((unsigned)grid);
-      if (sp2_enabled() && cmax == 151 && up <= kSpLanes / 2) {
-        // split rows: S2 lane pairs per phase, K columns per unit, G units per item
-        const int kk = env_int("SDR_SP2_K", 4);  // 4 (G 2) or 2 (G 4): A/B
-        const int K2 = kk == 2 ? 2 : 4, G2 = kk == 2 ? 4 : 2;
-        LpArgs c2 = b;
-        c2.S = (kSpLanes / 2) / up;
-        if (c2.S * K2 * G2 <= fit) {
-          c2.C = c2.S * K2 * G2 < np ? c2.S * K2 * G2 : np;
-          c2.nbat = (np + c2.C - 1) / c2.C;
-          c2.nitems = c2.nbat * nstreams;
-          const dim3 g2((unsigned)(c2.nitems < ncu ? c2.nitems : ncu)), blk2(kSpLanes + 128);
-          if (K2 == 2)
-            hipLaunchKernelGGL((resample_sp2<151, 2, 4>), g2, blk2, 0, st, c2);
-          else
-            hipLaunchKernelGGL((resample_sp2<151, 4, 2>), g2, blk2, 0, st, c2);
-          *err = hipGetLastError();
-          *state_done = true;
-          return true;
-        }
-      }
       if (lp_loader()) {
         const dim3 blk(kLpSlots + 64);
         if (cmax == 151) {

@@ -153,11 +153,9 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
 RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
                   (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                   (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
-# resample_sp2 (split tap rows), resample_lp with its loader wave and without, then resample_rs,
+# resample_lp with its loader wave (the default) and without, then resample_rs,
 # then the phase-major resample_pp
-RESAMPLE_KERNELS = {"sp2": {"SDR_RESAMPLE_SP2": "1"},
-                    "lpw": {"SDR_RESAMPLE_LOADER": "1", "SDR_RESAMPLE_SP2": "0"},
-                    "lp": {"SDR_RESAMPLE_LOADER": "0", "SDR_RESAMPLE_SP2": "0"},
+RESAMPLE_KERNELS = {"lpw": {"SDR_RESAMPLE_LOADER": "1"}, "lp": {"SDR_RESAMPLE_LOADER": "0"},
                     "rs": {"SDR_RESAMPLE_LP": "0"},
                     "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
 
@@ -195,7 +193,7 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
         assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
 
 
-@pytest.mark.parametrize("kernel", ["sp2", "lpw", "lp", "rs"])
+@pytest.mark.parametrize("kernel", ["lpw", "lp", "rs"])
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 8000), (147, 1280, 101, 100, 12800)])
 def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
     """Inf and NaN inputs (and in the carried state): every output equals the
