@@ -1076,6 +1076,201 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
 }
 #undef SDR_TRACE_AT
 
+// ------------------------------------------------ split-channel front end --
+// One channel of a lane's window: acc[r] = sum_k h[k] * w[HALO + D r - k] in
+// the reference's order (k ascending, product and sum rounded separately),
+// taps as SGPR operands in NPASS passes -- fir_tile's scan, one channel.
+template <int D, int T, int R, bool FMA>
+__device__ __forceinline__ void scan_one(const float* w, float (&acc)[R], const float* h) {
+  using G = Geom<D, T, R, true, 1>;
+  constexpr int NPASS = SDR_NPASS, KP = (T + NPASS - 1) / NPASS;
+  using hconst = const __attribute__((address_space(4))) float*;
+  const hconst hc = (hconst)h;
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+  float hs[KP];
+  static_for<0, NPASS>([&](auto pi) {
+    constexpr int k0 = decltype(pi)::value * KP;
+    constexpr int k1 = k0 + KP < T ? k0 + KP : T;
+#pragma unroll
+    for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
+#pragma unroll
+    for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
+    constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
+    constexpr int whi = G::HALO + D * (R - 1) - k0;
+    constexpr int clo = wlo / 4, chi = whi / 4;
+    float4 q0 = *reinterpret_cast<const float4*>(w + 4 * chi);
+    float4 q1 = q0;
+    if constexpr (chi - 1 >= clo) q1 = *reinterpret_cast<const float4*>(w + 4 * (chi - 1));
+    static_for<0, chi - clo + 1>([&](auto ci) {
+      constexpr int c = chi - decltype(ci)::value;
+      float4 n2 = q1;
+      if constexpr (c - 2 >= clo) n2 = *reinterpret_cast<const float4*>(w + 4 * (c - 2));
+      const float e[4] = {q0.x, q0.y, q0.z, q0.w};
+      static_for<0, 4>([&](auto ji) {
+        constexpr int j = 3 - decltype(ji)::value;
+        static_for<0, R>([&](auto ri) {
+          constexpr int r = decltype(ri)::value;
+          constexpr int k = G::HALO + D * r - (4 * c + j);
+          if constexpr (k >= k0 && k < k1) {
+            if constexpr (FMA)
+              acc[r] = __builtin_fmaf(hs[k - k0], e[j], acc[r]);
+            else
+              acc[r] = acc[r] + hs[k - k0] * e[j];
+          }
+        });
+      });
+      q0 = q1;
+      q1 = n2;
+#pragma unroll
+      for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  });
+}
+
+// fir_tile_sc: the fused f32 front end with the two channels of a tile on
+// two waves.  Wave 0 stages and scans I, wave 1 stages and scans Q, each in
+// its own 5,488-B slice; wave 1 hands its R outputs per lane to wave 0
+// through LDS (one barrier), wave 0 runs the discriminator and stores.  A
+// workgroup lives about as long as one channel's scan instead of two, with
+// half the staging registers per wave.  Same tiles, arithmetic, order,
+// outputs and state as fir_tile (src/filter.cpp:123-140, 85-102).
+template <int D, int T, int R, bool FMA = false>
+__global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __restrict__ h) {
+  constexpr int NW = 1, NTH = 64;
+  constexpr bool DEMOD = true;
+  constexpr Src SRC = Src::F32;
+  using G = Geom<D, T, R, DEMOD, NW>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // channel of this wave
+  const int lane = threadIdx.x & 63;
+  float* lds = smem + c * G::LDS_LEN;  // this channel's span
+  float* xch = smem + 2 * G::LDS_LEN;  // wave 1's outputs for wave 0
+  const long long n = a.n;
+  const long long nout = n / D;
+  const int ns = a.ns;
+  const int total = a.nstreams * a.tiles_per_stream;
+  // XCD slabs (fir_tile walk 1): workgroup b runs on XCD b % 8
+  const int per_xcd = (total + 7) / 8;
+  const int x = blockIdx.x & 7;
+  const int lin = x * per_xcd + (blockIdx.x >> 3);
+  if (lin >= min((x + 1) * per_xcd, total)) return;
+  TileRef tr = tile_ref<D, T, R, DEMOD, NW, 2, SRC>(a, lin);
+  if (c) {
+    tr.x0 = tr.x1;
+    tr.st0 = tr.st1;
+  }
+  float old_pi = 0.0f, old_pq = 0.0f;
+  if (c == 0 && tr.t == 0) {
+    using cf = const __attribute__((address_space(4))) float*;
+    const int s = __builtin_amdgcn_readfirstlane(tr.s);
+    old_pi = ((cf)a.prev0)[s];
+    old_pq = ((cf)a.prev1)[s];
+    // both read before the barrier below: wave 1 rewrites prev_Q after it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  using Stage = float4[G::FULL + 1];
+  Stage v;
+#pragma unroll
+  for (int i = 0; i <= G::FULL; ++i) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.ablate != 1) stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
+  stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds, lds, lane, v, v);
+  if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {
+    wave_sync();
+    edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, lane, n, ns, [&](int i, float v0, float) { lds[i] = v0; });
+  }
+  wave_sync();  // a wave reads only its own slice
+  const int lbase = D * R * lane;
+  float acc[R];
+  if (a.ablate == 2) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = lds[lbase + r];
+  } else {
+    scan_one<D, T, R, FMA>(lds + lbase, acc, h);
+  }
+  if (c == 1) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) xch[r * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (c == 0) {
+    float accQ[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) accQ[r] = xch[r * 64 + lane];
+    float pI = __shfl_up(acc[R - 1], 1, 64);
+    float pQ = __shfl_up(accQ[R - 1], 1, 64);
+    const bool first = tr.t == 0 && lane == 0;
+    if (first) {
+      pI = old_pi;
+      pQ = old_pq;
+    }
+    float d[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float ip = r ? acc[r - 1] : pI;
+      const float qp = r ? accQ[r - 1] : pQ;
+      d[r] = demod_one(acc[r], accQ[r], ip, qp);
+    }
+    const long long m0 = tr.m_start + (long long)R * lane;
+    float* o = a.out + (long long)tr.s * a.out_stride;
+    const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+    if (lane >= 1 || first) {
+      if (vec && m0 + R <= nout) {
+        if constexpr (R == 2) {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          if constexpr (SDR_OUT_NT)
+            __builtin_nontemporal_store(f2{d[0], d[1]}, reinterpret_cast<f2*>(o + m0));
+          else
+            *reinterpret_cast<f2*>(o + m0) = f2{d[0], d[1]};
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (m0 + r < nout) o[m0 + r] = d[r];
+      }
+    }
+  }
+  // state carry (tile 0): each wave its own channel, after every read of the old values
+  if (tr.t == 0) {
+    float* strip = lds;  // the scan is done with it
+    for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u * NTH + lane;
+        w[u] = j < G::STRIP ? edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, n - G::STRIP + j) : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u * NTH + lane;
+        if (j < G::STRIP) strip[j] = w[u];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    wave_sync();
+    if (lane == 0) {
+      // prev_c <- this channel's last decimated output (src/filter.cpp:100-101),
+      // recomputed in the reference's order from the strip
+      using hconst = const __attribute__((address_space(4))) float*;
+      const hconst hc = (hconst)h;
+      const float* sp = strip + (G::STRIP - D);
+      float y = 0.0f;
+#pragma unroll 8
+      for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
+      (c ? a.prev1 : a.prev0)[tr.s] = y;
+    }
+    if (ns <= G::STRIP) {
+      for (int j = lane; j < ns; j += NTH) tr.st0[j] = strip[G::STRIP - ns + j];
+    } else {
+      for (int j = lane; j < ns; j += NTH) tr.st0[j] = tr.x0[n - ns + j];
+    }
+  }
+}
+
 // ---------------------------------------------------------- generic path --
 // Any D / T / ns the tiled kernel is not instantiated for.  One thread per
 // output sample, same operation order; x~ read straight from global memory.
@@ -1214,6 +1409,31 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   return hipGetLastError();
 }
 
+// fir_tile_sc launch: one two-wave workgroup per tile, XCD slabs
+template <int D, int T, int R, bool FMA = false>
+hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
+  using G = Geom<D, T, R, true, 1>;
+  FirLaunch a = a0;
+  const long long nout = a.n / D;
+  a.tiles_per_stream = nout > G::E ? (int)((nout - G::E + G::ADV - 1) / G::ADV) : 1;
+  const long long total = (long long)a.tiles_per_stream * a.nstreams;
+  if (total <= 0 || total > 0x7fffffffLL - 8) return hipErrorInvalidValue;
+  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
+  a.ablate = ablate;
+  const long long per_xcd = (total + 7) / 8;
+  const size_t lds = (size_t)(2 * G::LDS_LEN + 64 * R) * sizeof(float);
+  hipLaunchKernelGGL((fir_tile_sc<D, T, R, FMA>), dim3((unsigned)(8 * per_xcd)), dim3(128), lds, st, a, h);
+  return hipGetLastError();
+}
+
+// The fused f32 front end runs fir_tile_sc (same box: 0.0978-0.0990 vs
+// 0.1015-0.1056 ms on cfg2, profiles/r03_ab/cfg2_split_channel.txt);
+// SDR_FIR_SC=0 selects fir_tile (read per launch, so a test runs both)
+bool sc_enabled() {
+  const char* e = std::getenv("SDR_FIR_SC");
+  return !e || std::atoi(e) != 0;
+}
+
 // Tile shape per decimation factor: R outputs per lane, one wave per
 // workgroup, taps in SGPRs (TM 1), waves per CU.  D*R must
 // be a multiple of 4 (aligned lane windows).  These are the measured best on
@@ -1255,6 +1475,8 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
         // the u8 wire format (VALU-bound: 2.4 B per pair) runs persistent
         // groups; f32 (HBM-bound) one tile per workgroup -- DESIGN.md 5.2
         case 10:
+          if constexpr (SRC == Src::F32)
+            if (sc_enabled()) return a.fma ? run_tile_sc<10, 101, 2, true>(a, h, st) : run_tile_sc<10, 101, 2>(a, h, st);
           return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 64)
                        : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, kPersistFused, 64);
         case 5:

@@ -23,8 +23,11 @@ def _blocks(a, block, nblk):
 
 # ------------------------------------------------------------ golden, host API
 
+@pytest.mark.parametrize("kernel", ["tile", "sc"])
 @pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
-def test_frontend_fused_golden(gpu_ctx, oracle, manifest, name):
+def test_frontend_fused_golden(gpu_ctx, oracle, manifest, monkeypatch, name, kernel):
+    """kernel: the fused f32 front end on fir_tile, or on fir_tile_sc (SDR_FIR_SC=1)."""
+    monkeypatch.setenv("SDR_FIR_SC", "1" if kernel == "sc" else "0")
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     I, Q = oracle.u8_to_planar(g["iq_u8"])
@@ -115,13 +118,15 @@ def test_fir_decim_vs_oracle(gpu_ctx, oracle, D, ntaps, ns, n):
 @pytest.mark.parametrize("D,n,ns", [(10, 5130, 100), (10, 5130, 150), (10, 2000, 200), (5, 4105, 100),
                                     (5, 4105, 128), (10, 110, 100), (10, 200, 180), (10, 130, 120),
                                     (10, 65530, 100), (10, 65550, 300)])
-def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, D, n, ns):
+@pytest.mark.parametrize("kernel", ["tile", "sc"])
+def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, monkeypatch, D, n, ns, kernel):
     """Fused front end (f32 and u8 wire) where the tiled kernel's edge
     handling matters: n % 4 != 0 (a chunk straddles the block end), state
     lengths below and above the kernel's staged strip, blocks barely longer
     than the state (the last output's inputs reach into the old state)."""
     from sdrhip.synth import fm_iq_u8
 
+    monkeypatch.setenv("SDR_FIR_SC", "1" if kernel == "sc" else "0")
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = fm_iq_u8(n * 3, seed=D * 100 + n + ns)
     st = {k: [np.zeros(ns, np.float32), np.zeros(ns, np.float32), np.zeros(2, np.float32)]
@@ -303,12 +308,14 @@ def _fm_streams(nstreams, n, seed=5):
     return np.stack([fm_iq_u8(n, seed=seed + s) for s in range(nstreams)])
 
 
-@pytest.mark.parametrize("src", ["f32", "u8"])
+@pytest.mark.parametrize("src", ["f32", "f32sc", "u8"])
 @pytest.mark.parametrize("D,n", [(10, 65540), (10, 5120), (5, 40960)])
-def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, src, D, n):
+def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, src, D, n):
     """nstreams independent streams x 3 consecutive blocks through the
-    device-resident batched call; every stream checked against the oracle."""
+    device-resident batched call; every stream checked against the oracle.
+    f32sc: the f32 call on fir_tile_sc (SDR_FIR_SC=1)."""
     sdrhip = built_lib
+    monkeypatch.setenv("SDR_FIR_SC", "1" if src == "f32sc" else "0")
     nstreams, nblk = 6, 3
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = _fm_streams(nstreams, n * nblk)
