@@ -1136,11 +1136,10 @@ __device__ __forceinline__ void scan_one(const float* w, float (&acc)[R], const 
 // workgroup lives about as long as one channel's scan instead of two, with
 // half the staging registers per wave.  Same tiles, arithmetic, order,
 // outputs and state as fir_tile (src/filter.cpp:123-140, 85-102).
-template <int D, int T, int R, bool FMA = false>
+template <int D, int T, int R, Src SRC, bool FMA = false>
 __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __restrict__ h) {
   constexpr int NW = 1, NTH = 64;
   constexpr bool DEMOD = true;
-  constexpr Src SRC = Src::F32;
   using G = Geom<D, T, R, DEMOD, NW>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // channel of this wave
@@ -1175,10 +1174,27 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.ablate != 1) stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
-  stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds, lds, lane, v, v);
+  if constexpr (SRC == Src::F32) {
+    stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds, lds, lane, v, v);
+  } else {
+    // u8 wire format: both waves load the interleaved bytes (I0 Q0 I1 Q1 | I2 Q2 I3 Q3
+    // per chunk; the second read hits L2) and unpack their own channel
+    auto put = [&](int i, const float4& w) __attribute__((always_inline)) {
+      const uint32_t bx = __float_as_uint(w.x), by = __float_as_uint(w.y);
+      if (c == 0)
+        *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(u8_byte_to_f32<0>(bx), u8_byte_to_f32<2>(bx),
+                                                              u8_byte_to_f32<0>(by), u8_byte_to_f32<2>(by));
+      else
+        *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(u8_byte_to_f32<1>(bx), u8_byte_to_f32<3>(bx),
+                                                              u8_byte_to_f32<1>(by), u8_byte_to_f32<3>(by));
+    };
+#pragma unroll
+    for (int it = 0; it < G::FULL; ++it) put(lane + it * NTH, v[it]);
+    if (G::REM && lane < G::REM) put(lane + G::FULL * NTH, v[G::FULL]);
+  }
   if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {
     wave_sync();
-    edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, lane, n, ns, [&](int i, float v0, float) { lds[i] = v0; });
+    edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, lane, n, ns, [&](int i, float v0, float) { lds[i] = v0; }, c);
   }
   wave_sync();  // a wave reads only its own slice
   const int lbase = D * R * lane;
@@ -1242,7 +1258,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int j = j0 + u * NTH + lane;
-        w[u] = j < G::STRIP ? edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, n - G::STRIP + j) : 0.0f;
+        w[u] = j < G::STRIP ? edge_at<SRC>(tr.x0, tr.iq, c, tr.st0, ns, n, n - G::STRIP + j) : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -1266,7 +1282,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     if (ns <= G::STRIP) {
       for (int j = lane; j < ns; j += NTH) tr.st0[j] = strip[G::STRIP - ns + j];
     } else {
-      for (int j = lane; j < ns; j += NTH) tr.st0[j] = tr.x0[n - ns + j];
+      for (int j = lane; j < ns; j += NTH) tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, c, n - ns + j);
     }
   }
 }
@@ -1410,7 +1426,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
 }
 
 // fir_tile_sc launch: one two-wave workgroup per tile, XCD slabs
-template <int D, int T, int R, bool FMA = false>
+template <int D, int T, int R, Src SRC, bool FMA = false>
 hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
   using G = Geom<D, T, R, true, 1>;
   FirLaunch a = a0;
@@ -1422,7 +1438,7 @@ hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
   a.ablate = ablate;
   const long long per_xcd = (total + 7) / 8;
   const size_t lds = (size_t)(2 * G::LDS_LEN + 64 * R) * sizeof(float);
-  hipLaunchKernelGGL((fir_tile_sc<D, T, R, FMA>), dim3((unsigned)(8 * per_xcd)), dim3(128), lds, st, a, h);
+  hipLaunchKernelGGL((fir_tile_sc<D, T, R, SRC, FMA>), dim3((unsigned)(8 * per_xcd)), dim3(128), lds, st, a, h);
   return hipGetLastError();
 }
 
@@ -1431,6 +1447,12 @@ hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
 // SDR_FIR_SC=0 selects fir_tile (read per launch, so a test runs both)
 bool sc_enabled() {
   const char* e = std::getenv("SDR_FIR_SC");
+  return !e || std::atoi(e) != 0;
+}
+// the u8 wire path on fir_tile_sc too (cfg2u8 0.0806-0.0813 -> 0.0785-0.0788 ms,
+// mono0 -1 %); SDR_FIR_SC_U8=0 selects fir_tile_grp
+bool sc_u8_enabled() {
+  const char* e = std::getenv("SDR_FIR_SC_U8");
   return !e || std::atoi(e) != 0;
 }
 
@@ -1472,11 +1494,11 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
       // SDR_ARITH_FMA: instantiated for the fused kernels; any other shape
       // runs the exact arithmetic (inside the tolerance)
       switch (a.D) {
-        // the u8 wire format (VALU-bound: 2.4 B per pair) runs persistent
-        // groups; f32 (HBM-bound) one tile per workgroup -- DESIGN.md 5.2
+        // fir_tile_sc by default (both sources); otherwise the u8 wire format
+        // runs persistent groups, f32 one tile per workgroup -- DESIGN.md 5.2
         case 10:
-          if constexpr (SRC == Src::F32)
-            if (sc_enabled()) return a.fma ? run_tile_sc<10, 101, 2, true>(a, h, st) : run_tile_sc<10, 101, 2>(a, h, st);
+          if (SRC == Src::F32 ? sc_enabled() : sc_u8_enabled())
+            return a.fma ? run_tile_sc<10, 101, 2, SRC, true>(a, h, st) : run_tile_sc<10, 101, 2, SRC>(a, h, st);
           return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 64)
                        : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, kPersistFused, 64);
         case 5:

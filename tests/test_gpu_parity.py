@@ -38,8 +38,10 @@ def test_frontend_fused_golden(gpu_ctx, oracle, manifest, monkeypatch, name, ker
         assert_bits(np.concatenate([si, sq, prev]), g["states"][b], f"{name} states[{b}]")
 
 
+@pytest.mark.parametrize("kernel", ["grp", "sc"])
 @pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
-def test_frontend_u8_golden(gpu_ctx, manifest, name):
+def test_frontend_u8_golden(gpu_ctx, manifest, monkeypatch, name, kernel):
+    monkeypatch.setenv("SDR_FIR_SC_U8", "1" if kernel == "sc" else "0")
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     si, sq, prev = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
@@ -127,6 +129,7 @@ def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, monkeypatch, D, n, ns, k
     from sdrhip.synth import fm_iq_u8
 
     monkeypatch.setenv("SDR_FIR_SC", "1" if kernel == "sc" else "0")
+    monkeypatch.setenv("SDR_FIR_SC_U8", "1" if kernel == "sc" else "0")
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = fm_iq_u8(n * 3, seed=D * 100 + n + ns)
     st = {k: [np.zeros(ns, np.float32), np.zeros(ns, np.float32), np.zeros(2, np.float32)]
@@ -308,7 +311,7 @@ def _fm_streams(nstreams, n, seed=5):
     return np.stack([fm_iq_u8(n, seed=seed + s) for s in range(nstreams)])
 
 
-@pytest.mark.parametrize("src", ["f32", "f32sc", "u8"])
+@pytest.mark.parametrize("src", ["f32", "f32sc", "u8", "u8sc"])
 @pytest.mark.parametrize("D,n", [(10, 65540), (10, 5120), (5, 40960)])
 def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, src, D, n):
     """nstreams independent streams x 3 consecutive blocks through the
@@ -316,6 +319,8 @@ def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, src
     f32sc: the f32 call on fir_tile_sc (SDR_FIR_SC=1)."""
     sdrhip = built_lib
     monkeypatch.setenv("SDR_FIR_SC", "1" if src == "f32sc" else "0")
+    monkeypatch.setenv("SDR_FIR_SC_U8", "1" if src == "u8sc" else "0")
+    src = src[:-2] if src.endswith("sc") else src
     nstreams, nblk = 6, 3
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = _fm_streams(nstreams, n * nblk)
