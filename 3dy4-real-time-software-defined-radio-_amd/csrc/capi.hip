@@ -10,7 +10,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "sdr_common.hpp"
 #include "sdr_hip.h"
@@ -34,6 +37,9 @@ struct sdr_ctx {
   // live graphs recorded on this context: they hold pointers into buf[], so
   // scratch() refuses to reallocate while any exists (or while capturing)
   int graphs = 0;
+  // sdr_ctx_pin_scratch: a caller's own capture (e.g. torch.cuda.graph on the
+  // stream given to sdr_ctx_set_stream) holds the buffers too
+  bool pinned = false;
   bool grow_refused = false;
   std::string err;
 };
@@ -87,7 +93,7 @@ bool capturing(hipStream_t s) {
 void* scratch(sdr_ctx* c, int slot, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (c->cap[slot] >= bytes) return c->buf[slot];
-  if (c->graphs > 0 || capturing(c->cur) || capturing(c->side)) {
+  if (c->graphs > 0 || c->pinned || capturing(c->cur) || capturing(c->side)) {
     c->grow_refused = true;
     return nullptr;
   }
@@ -114,8 +120,9 @@ int scratch_fail(sdr_ctx* c, const char* what) {
   if (c->grow_refused) {
     c->grow_refused = false;
     return fail(c, SDR_EINVAL,
-                "%s: scratch would have to grow while a graph recorded on this context is alive or being captured "
-                "(run one direct call of the largest shape before capturing, or destroy the graphs first)",
+                "%s: scratch would have to grow while a graph recorded on this context is alive or being captured, "
+                "or while it is pinned (run one direct call of the largest shape before capturing, or destroy the "
+                "graphs / unpin first)",
                 what);
   }
   return fail(c, SDR_ENOMEM, "%s", what);
@@ -169,6 +176,30 @@ int device_cu_count() {
   int n = cache[dev].load(std::memory_order_relaxed);
   if (n > 0) return n;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+int device_lds_bytes() {
+  // LDS per CU (160 KiB on gfx950), cached per device like the CU count
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || n <= 0)
+    n = 65536;  // the smallest LDS a CDNA CU has: never over-subscribe
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+int device_grid_y_max() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMaxGridDimY, dev) != hipSuccess || n <= 0) n = 65535;
   cache[dev].store(n, std::memory_order_relaxed);
   return n;
 }
@@ -248,6 +279,12 @@ int sdr_ctx_set_arith(sdr_ctx* c, int mode) {
   if (!c) return SDR_EINVAL;
   if (mode != SDR_ARITH_EXACT && mode != SDR_ARITH_FMA) return fail(c, SDR_EINVAL, "unknown arithmetic mode %d", mode);
   c->arith = mode;
+  return SDR_OK;
+}
+
+int sdr_ctx_pin_scratch(sdr_ctx* c, int pinned) {
+  if (!c) return SDR_EINVAL;
+  c->pinned = pinned != 0;
   return SDR_OK;
 }
 
@@ -634,6 +671,10 @@ struct sdr_resample_plan {
   int up = 0, down = 0, ntaps = 0;
   const float* h = nullptr;
   float* tables = nullptr;  // resample_lp's tables, or nullptr when the shape takes another kernel
+  // one event per stream that launched with the tables (recorded after each
+  // direct launch): destroy waits for exactly those, not the whole device
+  std::mutex mu;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
 };
 
 int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int ntaps, sdr_resample_plan** out) {
@@ -678,8 +719,12 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
   if (rc) return rc;
   if (p) {
     if (p->tables) {
-      // every stream that used the plan, not only the current one
-      (void)hipDeviceSynchronize();
+      // every stream that used the plan, not only the current one (graphs
+      // recorded with the plan must be destroyed before it, sdr_hip.h)
+      for (auto& u : p->uses) {
+        (void)hipEventSynchronize(u.second);
+        (void)hipEventDestroy(u.second);
+      }
       (void)hipFree(p->tables);
     }
     delete p;
@@ -690,7 +735,20 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
 int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const float* x, long long n, int nstreams,
                               long long x_stride, float* state, int ns, float* y, long long y_stride) {
   if (!p) return fail(c, SDR_EINVAL, "null plan");
-  return resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->tables);
+  const int rc = resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride,
+                              p->tables);
+  if (rc || !p->tables || capturing(c->cur)) return rc;
+  auto* pm = const_cast<sdr_resample_plan*>(p);
+  std::lock_guard<std::mutex> lk(pm->mu);
+  hipEvent_t ev = nullptr;
+  for (auto& u : pm->uses)
+    if (u.first == c->cur) ev = u.second;
+  if (!ev) {
+    SDR_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    pm->uses.emplace_back(c->cur, ev);
+  }
+  SDR_HIP(c, hipEventRecord(ev, c->cur));
+  return SDR_OK;
 }
 
 int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,

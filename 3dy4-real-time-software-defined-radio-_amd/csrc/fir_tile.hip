@@ -1378,8 +1378,10 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   static const int persist_env = env_int("SDR_FIR_PERSIST", -1);  // A/B
   if (persist_env >= 0) persist = persist_env != 0;
   if (persist) {
-    constexpr long long kLds = 163840 - 64;  // a CU's LDS, less the claim counter
+    // a CU's LDS (160 KiB on gfx950, read from the device), less the claim counter
+    const long long kLds = (long long)device_lds_bytes() - 64;
     constexpr long long slice = (long long)G::SMEM * sizeof(float);
+    if (kLds < slice) return hipErrorInvalidConfiguration;
     static const int wpg_env = env_int("SDR_FIR_WPG", 0);  // timing experiments
     long long wpg = std::min<long long>(16, kLds / slice);
     if (wpg_env > 0) wpg = std::min<long long>(wpg, wpg_env);
@@ -1449,12 +1451,12 @@ bool sc_enabled() {
   const char* e = std::getenv("SDR_FIR_SC");
   return !e || std::atoi(e) != 0;
 }
-// the u8 wire path on fir_tile_sc (SDR_FIR_SC_U8=1; cfg2u8 0.0806-0.0813 ->
-// 0.0785-0.0788 ms, mono0 -1 % on one box, its parity tests green; not yet
-// the default: the full GPU suite has not run with it)
+// the u8 wire path on fir_tile_sc too (cfg2u8 0.0806-0.0813 -> 0.0785-0.0788
+// ms, mono0 -1 % on one box); SDR_FIR_SC_U8=0 selects the persistent
+// fir_tile_grp (read per launch, so a test runs both)
 bool sc_u8_enabled() {
   const char* e = std::getenv("SDR_FIR_SC_U8");
-  return e && std::atoi(e) != 0;
+  return !e || std::atoi(e) != 0;
 }
 
 // Tile shape per decimation factor: R outputs per lane, one wave per
@@ -1495,8 +1497,8 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
       // SDR_ARITH_FMA: instantiated for the fused kernels; any other shape
       // runs the exact arithmetic (inside the tolerance)
       switch (a.D) {
-        // f32: fir_tile_sc by default; the u8 wire format runs persistent
-        // groups unless SDR_FIR_SC_U8=1 -- DESIGN.md 4.1, 5.2
+        // fir_tile_sc by default (SDR_FIR_SC=0 / SDR_FIR_SC_U8=0: fir_tile,
+        // the u8 wire format on persistent groups) -- DESIGN.md 4.1, 5.2
         case 10:
           if (SRC == Src::F32 ? sc_enabled() : sc_u8_enabled())
             return a.fma ? run_tile_sc<10, 101, 2, SRC, true>(a, h, st) : run_tile_sc<10, 101, 2, SRC>(a, h, st);

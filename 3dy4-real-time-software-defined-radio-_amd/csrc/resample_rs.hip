@@ -646,24 +646,32 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   // resample_lp: the staging buffer must hold at least one column's span
   const int base0 = -(((cmax - 1) + 3) / 4 * 4);
   const int qmax = (int)((long long)(up - 1) * down / up);
-  const bool use_lp = lp_enabled() && up <= kLpSlots && (long long)up * down < (1LL << 31) &&
-                      qmax + 1 - base0 + 4 <= kLpBuf && ns <= kLpSlots;
+  bool use_lp = lp_enabled() && up <= kLpSlots && (long long)up * down < (1LL << 31) &&
+                qmax + 1 - base0 + 4 <= kLpBuf && ns <= kLpSlots;
+  const int np = (int)((ny + up - 1) / up);
+  // resample_lp's columns per item: S*K chains, bounded by the staging buffer
+  const int lpS = kLpSlots / up;
+  const int lpK = (np <= 4 * lpS) ? 4 : 7;
+  int lpC = lpS * lpK;
+  {
+    const long long fit = (kLpBuf - (qmax + 1 - base0) - 4) / down + 1;
+    if (lpC > fit) lpC = (int)fit;
+    if (lpC > np) lpC = np;
+    if (lpC < 1) lpC = 1;
+  }
+  // resample_lp commits a stream's new state in its first item, at the top of
+  // that item's iteration; that is only safe when the first item is the ONLY
+  // reader of the old state, i.e. the second item's span starts at p >= 0
+  // (up = 128, down = 4 gives C = 21, P0 = 21*4 - 152 < 0).
+  if (use_lp && np > lpC && (long long)lpC * down + base0 < 0) use_lp = false;
   // resample_rs: the ring must hold a group's whole window plus the next group's new inputs
   const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
   const long long step = ((long long)kRsPG * down + up - 1) / up + 8;
   if (!use_lp && (!rs_enabled() || span + step > kRsRing)) return false;
   static const int ablate = env_int("SDR_ABLATE", 0);
   const int ncu = device_cu_count();
-  const int np = (int)((ny + up - 1) / up);
   if (use_lp) {
-    // columns per item: S*K chains, bounded by the staging buffer
-    const int S = kLpSlots / up;
-    const int K = (np <= 4 * S) ? 4 : 7;
-    int C = S * K;
-    const long long fit = (kLpBuf - (qmax + 1 - base0) - 4) / down + 1;
-    if (C > fit) C = (int)fit;
-    if (C > np) C = np;
-    if (C < 1) C = 1;
+    const int S = lpS, K = lpK, C = lpC;
     {
       LpArgs b;
       b.x = x;

@@ -65,6 +65,8 @@ __device__ __forceinline__ float u8_byte_to_f32(uint32_t w) {
 // (the launchers run concurrently from several host threads: the drop-in's
 // two threads per block, bench.py's one thread per GPU).
 int device_cu_count();
+int device_lds_bytes();  // LDS bytes per CU of the current device
+int device_grid_y_max();  // grid y limit of the current device (kernels put streams on y)
 // Integer environment switch (timing experiments), `dflt` when unset.
 int env_int(const char* name, int dflt);
 

@@ -260,7 +260,9 @@ hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, lon
   // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests);
   // SDR_PLL_GUARD=0 evaluates the input check inside the recurrence (A/B)
   const int fast = env_int("SDR_PLL_FAST", 1);
-  const bool pre = guard && nchunk > 0 && env_int("SDR_PLL_GUARD", 1) != 0;
+  // (the pre-pass puts the streams on grid y: past the device's grid-y limit
+  // the recurrence evaluates the guard itself -- same bits)
+  const bool pre = guard && nchunk > 0 && env_int("SDR_PLL_GUARD", 1) != 0 && nstreams <= device_grid_y_max();
   if (fast && pre) {
     hipLaunchKernelGGL(pll_guard_kernel, dim3((unsigned)((nchunk + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0,
                        st, in, nstreams, in_stride, guard, nchunk);

@@ -55,6 +55,7 @@ _SIGS = {
     "sdr_ctx_synchronize": [_vp],
     "sdr_ctx_set_arith": [_vp, _i],
     "sdr_ctx_set_stereo_fork": [_vp, _i],
+    "sdr_ctx_pin_scratch": [_vp, _i],
     "sdr_ctx_last_error": [_vp],
     "sdr_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "sdr_dev_free": [_vp, _vp],
@@ -271,6 +272,11 @@ class Context:
         """stereo_pcm_u8_dev's launch order: FORK_AUTO (side branch on a
         second stream at <= CUs/4 PLL waves), FORK_SERIAL or FORK_SIDE."""
         self._check(lib().sdr_ctx_set_stereo_fork(self._c, mode), "set_stereo_fork")
+
+    def pin_scratch(self, pinned: bool = True):
+        """Refuse scratch growth (SDR_EINVAL) while pinned: for graphs the
+        caller captures itself on this context's stream (sdr_ctx_pin_scratch)."""
+        self._check(lib().sdr_ctx_pin_scratch(self._c, int(bool(pinned))), "pin_scratch")
 
     def set_stream(self, hip_stream: int | None):
         """Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""

@@ -107,6 +107,9 @@ def parse(argv=None):
     ap.add_argument("--batches", type=int, default=2, help="distinct input batches the steps cycle over")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per replayed HIP graph")
     ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
+    ap.add_argument("--sustain-seconds", type=float, default=3.0,
+                    help="after the timed window, time this many seconds of back-to-back steps (the "
+                         "`sustained` field: a receiver runs the block loop continuously); 0 skips it")
     return ap.parse_args(argv)
 
 
@@ -461,6 +464,15 @@ class Job:
             barrier()
         return e0.elapsed_time(e1), wall
 
+    def sustained(self, seconds: float, ms_per_step: float, barrier=None):
+        """Steady state: enough back-to-back steps (whole graph replays) to fill
+        `seconds` of device time at the timed window's rate, enqueued at once
+        between HIP events.  Returns (ms_events, steps)."""
+        gs = self.graph[1] if self.graph is not None else 1
+        k = max(gs, int(np.ceil(seconds * 1e3 / max(ms_per_step, 1e-6) / gs)) * gs)
+        ms, _ = self.timed(k, barrier)
+        return ms, k
+
     def close(self):
         if self.graph is not None:
             self.graph[0].close()
@@ -485,6 +497,8 @@ def run_device(cfg_name, device, seed, args, barrier=None, side=True):
             job.capture(args.graph_steps)
         job.warm(0, args.warm_seconds)
         res["ms"], res["wall"] = job.timed(args.steps, barrier)
+        if args.sustain_seconds > 0:
+            res["sus_ms"], res["sus_steps"] = job.sustained(args.sustain_seconds, res["ms"] / args.steps, barrier)
         # Side measurement (fused front end, exact run only): the same launches
         # under SDR_ARITH_FMA -- one fused multiply-add per tap, not the
         # reference's bits (tolerance-tested); never `value`.
@@ -579,6 +593,7 @@ def main(argv=None):
         results.sort(key=lambda r: r["device"])  # stable: rehearsal lists may repeat a device
         rank, world = 0, len(devs)
         per_ms = [r["ms"] for r in results]
+        sus = [(r.get("sus_ms", 0.0), r.get("sus_steps", 0)) for r in results]
         distinct = len(set(devs))
         wall = max(r["wall"] for r in results)
     else:
@@ -591,8 +606,9 @@ def main(argv=None):
         try:
             r = run_device(args.config, plan["devices"][0], 1234 + 7919 * rank, args, barrier=dist.barrier,
                            side=False)
-            t = torch.tensor([r["ms"], r["wall"]], dtype=torch.float64)
-            allt = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+            t = torch.tensor([r["ms"], r["wall"], r.get("sus_ms", 0.0), r.get("sus_steps", 0)],
+                             dtype=torch.float64)
+            allt = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
             dist.all_gather(allt, t)
         finally:
             dist.destroy_process_group()
@@ -600,10 +616,25 @@ def main(argv=None):
         distinct = world
         per_ms = [float(x[0]) for x in allt]
         wall = max(float(x[1]) for x in allt)
+        sus = [(float(x[2]), int(x[3])) for x in allt]
 
     job = results[0]["job"]
     agg = aggregate(per_ms, job["units"], args.steps)
     roof = roofline(job, agg["ms_per_step"], args.config, args.arith)
+    sustained = None
+    if args.sustain_seconds > 0 and all(k > 0 for _, k in sus):
+        # devices may pick different step counts (each fills the same seconds at its
+        # own rate): all devices' units over the slowest device's elapsed time
+        sms = max(m for m, _ in sus)
+        sval = job["units"] * sum(k for _, k in sus) / (sms * 1e-3) / 1e6
+        sstep = max(m / k for m, k in sus)
+        sroof = roofline(job, sstep, args.config, args.arith)
+        sustained = {"seconds": round(sms * 1e-3, 3), "steps": [k for _, k in sus],
+                     "ms_per_step": round(sstep, 5), "value": round(sval, 1),
+                     "frac": sroof["frac"], "bound": sroof["bound"], "hbm_frac": sroof["hbm_frac"],
+                     "valu_frac": sroof["valu_frac"],
+                     "note": "back-to-back steps right after the timed window, one HIP-event pair around all "
+                             "of them (steady state of the block loop); reported beside `value`, never as it"}
     fma_variant = None
     if len(results) == 1 and "fma_ms" in results[0]:
         fms = results[0]["fma_ms"] / args.steps
@@ -635,6 +666,7 @@ def main(argv=None):
                         "ms_per_step": [round(m / args.steps, 4) for m in per_ms]},
             "roofline": roof, "cpu_baseline": cpu,
             **({"tolerance": job["tolerance"]} if job["tolerance"] else {}),
+            **({"sustained": sustained} if sustained else {}),
             **({"fma_variant": fma_variant} if fma_variant else {}),
             "wall_ms": round(wall * 1e3, 3),
         }

@@ -121,7 +121,15 @@ int sdr_event_destroy(sdr_ctx *ctx, sdr_event *ev);
  * with, so while any graph of the context is alive (or a capture is in
  * progress) a call that would need larger scratch fails with SDR_EINVAL
  * instead of reallocating under the graph: make one direct call of the
- * largest shape before capturing, or destroy the graphs first. */
+ * largest shape before capturing, or destroy the graphs first.
+ * The library only knows the graphs sdr_graph_end made.  A caller that
+ * captures the context's stream itself (after sdr_ctx_set_stream, e.g. with
+ * torch.cuda.graph) must size the scratch by one direct call of the largest
+ * shape first and then pin it with sdr_ctx_pin_scratch(ctx, 1) for as long as
+ * its graphs live: while pinned, growth is refused (SDR_EINVAL) instead of
+ * freeing buffers the caller's graph still replays.  sdr_ctx_pin_scratch(ctx,
+ * 0) unpins. */
+int sdr_ctx_pin_scratch(sdr_ctx *ctx, int pinned);
 typedef struct sdr_graph sdr_graph;
 int sdr_graph_begin(sdr_ctx *ctx);
 int sdr_graph_end(sdr_ctx *ctx, sdr_graph **graph);
@@ -194,7 +202,10 @@ int sdr_resample_f32_dev(sdr_ctx *ctx, int up, int down, const float *x, long lo
  * (src/project.cpp:262-266 designs them once), so the per-block call is a
  * single launch.  h is read at creation by that kernel and at each call by
  * the fallback kernels (other shapes): it must not change while the plan
- * lives.  Same outputs, state and preconditions as sdr_resample_f32_dev. */
+ * lives.  Same outputs, state and preconditions as sdr_resample_f32_dev.
+ * sdr_resample_plan_destroy waits for the last direct call on every stream
+ * that used the plan (one event per stream), not for the whole device; graphs
+ * that recorded calls with the plan must be destroyed before it. */
 typedef struct sdr_resample_plan sdr_resample_plan;
 int sdr_resample_plan_create(sdr_ctx *ctx, int up, int down, const float *h, int ntaps,
                              sdr_resample_plan **plan);

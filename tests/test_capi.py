@@ -140,3 +140,47 @@ def test_sdr_project_usage_without_gpu(built_lib):
     r = subprocess.run([prog, "7", "mono"], capture_output=True)
     assert r.returncode == 1 and b"Wrong mode: 7" in r.stderr
 
+
+
+@pytest.mark.gpu
+def test_scratch_growth_refused_then_recovered(built_lib, oracle):
+    """Grow-only scratch under graphs (include/sdr_hip.h): while a
+    graph recorded on the context is alive, or while the caller has pinned the
+    scratch for its own capture (sdr_ctx_pin_scratch), a call that needs larger
+    scratch fails with SDR_EINVAL instead of freeing buffers a graph replays;
+    after sdr_graph_destroy / unpinning the same call grows and is bit-exact."""
+    sdrhip = built_lib
+    h = oracle.taps_lpf(2.4e6, 100e3, 101, 1)
+    rng = np.random.default_rng(12)
+    small, big = rng.standard_normal(1000).astype(np.float32), rng.standard_normal(50000).astype(np.float32)
+    with sdrhip.Context(0) as ctx:
+        A = sdrhip.DeviceArray
+        st = np.zeros(100, np.float32)
+        ctx.fir_block(small, h, st)  # sizes the host-call scratch for 1,000 samples
+        d_x, d_h = A.from_numpy(ctx, small), A.from_numpy(ctx, h)
+        d_st, d_y = A(ctx, 400), A(ctx, 4000)
+        d_st.fill(0)
+        ctx.fir_block_dev(d_x, 1000, 1, 1000, d_h, 101, d_st, 100, d_y, 1000)
+        ctx.synchronize()
+        for hold in ("graph", "pin"):
+            if hold == "graph":
+                g = ctx.capture(lambda: ctx.fir_block_dev(d_x, 1000, 1, 1000, d_h, 101, d_st, 100, d_y, 1000))
+            else:
+                ctx.pin_scratch(True)
+            st_big = np.zeros(100, np.float32)
+            with pytest.raises(sdrhip.SdrError) as ei:
+                ctx.fir_block(big, h, st_big)
+            assert ei.value.code == sdrhip.SDR_EINVAL and "scratch" in ctx.last_error()
+            if hold == "graph":
+                g.launch()  # the graph still replays its own (unchanged) buffers
+                ctx.synchronize()
+                g.close()
+            else:
+                ctx.pin_scratch(False)
+            st_big = np.zeros(100, np.float32)
+            st_ref = np.zeros(100, np.float32)
+            got = ctx.fir_block(big, h, st_big)
+            assert np.array_equal(got.view(np.uint32), oracle.fir_block(big, h, st_ref).view(np.uint32))
+            assert np.array_equal(st_big, st_ref)
+            small = big  # the next round must grow past the new size again
+            big = rng.standard_normal(len(big) * 3).astype(np.float32)

@@ -13,8 +13,13 @@ benchmark times (f32 planar `frontend_dev`, state carried across steps):
   src/filter.cpp:139;
 * config 5: the 1024-tap FIR over 2 x 1,048,576 samples, windows at the
   start (real state), middle and end checked against the oracle (each
-  window's state is the preceding 1,023 inputs, src/filter.cpp:82).
+  window's state is the preceding 1,023 inputs, src/filter.cpp:82); its
+  fp16 arm over the whole 2 x 1,048,576 within the stated tolerance;
+* config 3: the resampler plan at the bench's launch (1,024 x 65,600, the
+  real 22,197-tap design), two steps, every stream bitwise.
 """
+import concurrent.futures as cf
+
 import numpy as np
 import pytest
 
@@ -211,3 +216,76 @@ def test_cfg5_full_windows(gpu_ctx, oracle, built_lib):
             want = oracle.fir_block(x[c, a:a + W], h, x[c, a - (T - 1):a].copy())
             assert_bits(y[c, a:a + W], want, f"channel {c} window at {a}")
     assert_bits(d_st.download().reshape(2, T - 1), x[:, n - (T - 1):], "state")
+
+
+def test_cfg3_full_plan_two_steps(gpu_ctx, oracle, built_lib):
+    """BASELINE config 3 exactly as bench.py launches it: 1,024 streams x
+    65,600 samples through a resampler plan built from the real
+    impulseResponseLPF(240e3*147, 16e3, 22197, 147) taps (151 per phase, S =
+    150), two consecutive steps with the state carried.  EVERY stream's
+    12,054 outputs and carried state bitwise against the oracle
+    (src/filter.cpp:142-173) -- the workgroup item split at 1,024 streams."""
+    sdrhip = built_lib
+    S, n, up, down, T, ns = 1024, 65600, 147, 800, 151 * 147, 150
+    ny = sdrhip.resample_out_len(up, down, n)
+    assert ny == 12054
+    h = oracle.taps_lpf(240e3 * 147, 16e3, T, 147)
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    plan = gpu_ctx.resample_plan(up, down, d_h, T)
+    d_st = _dev(sdrhip, gpu_ctx, np.zeros((S, ns), np.float32))
+    d_y = sdrhip.DeviceArray(gpu_ctx, S * ny * 4)
+    ors = [np.zeros(ns, np.float32) for _ in range(S)]
+    try:
+        for step, seed in enumerate((331, 332)):
+            d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, seed)
+            d_Q.free()
+            d_y.fill(0xFF)
+            plan.resample_dev(d_I, n, S, n, d_st, ns, d_y, ny)
+            gpu_ctx.synchronize()
+            got = d_y.download().reshape(S, ny)
+            x = d_I.download().reshape(S, n)
+            with cf.ThreadPoolExecutor(16) as ex:  # C behind ctypes: the GIL is released
+                want = np.stack(list(ex.map(lambda s: oracle.resample(up, down, x[s], h, ors[s]), range(S))))
+            assert_bits(got, want, f"step {step}: all {S} streams")
+            assert_bits(d_st.download().reshape(S, ns), np.stack(ors), f"step {step}: state (all streams)")
+            d_I.free()
+    finally:
+        plan.close()
+
+
+def test_cfg5h_full_f16_tolerance(gpu_ctx, oracle, built_lib):
+    """BASELINE config 5's fp16 arm at full size (2 x 1,048,576 samples, the
+    1024-tap LPF, fp16 storage, fp32 v_dot2 accumulation): every output within
+    2^-9 * sum|h| * max|x| of the exact fp32 reference (src/filter.cpp:66-83),
+    and within fp32 accumulation error of the exact sum over the fp16-rounded
+    operands; the fp16 state is the last 1,023 inputs exactly."""
+    from scipy.signal import oaconvolve
+
+    sdrhip = built_lib
+    n, T = 1048576, 1024
+    ns = T - 1
+    h = oracle.taps_lpf(2.4e6, 100e3, T, 1)
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, 1, n, 56)
+    x = np.stack([d_I.download(), d_Q.download()])
+    d_I.free()
+    d_Q.free()
+    x16 = x.astype(np.float16)
+    st0 = np.random.default_rng(5).uniform(-0.7, 0.7, (2, ns)).astype(np.float16)
+    d_x, d_st = _dev(sdrhip, gpu_ctx, x16), _dev(sdrhip, gpu_ctx, st0)
+    d_y = sdrhip.DeviceArray(gpu_ctx, 2 * n * 4)
+    gpu_ctx.fir_block_f16_dev(d_x, n, 2, n, d_h, T, d_st, ns, d_y, n)
+    gpu_ctx.synchronize()
+    got = d_y.download().reshape(2, n).astype(np.float64)
+    hh = h.astype(np.float16).astype(np.float64)
+    for c in range(2):
+        want = oracle.fir_block(x[c], h, st0[c].astype(np.float32))
+        scale = float(np.abs(h).sum()) * float(np.abs(x[c]).max())
+        err = np.abs(got[c] - want).max()
+        assert err <= 2.0 ** -9 * scale, f"channel {c}: {err:.3g} > 2^-9 * {scale:.3g}"
+        xs = np.concatenate([st0[c].astype(np.float64), x16[c].astype(np.float64)])
+        exact = oaconvolve(xs, hh)[ns:ns + n]
+        bound = T * 2.0 ** -23 * oaconvolve(np.abs(xs), np.abs(hh))[ns:ns + n] + 1e-9
+        worst = np.max(np.abs(got[c] - exact) - bound)
+        assert worst <= 0, f"channel {c}: off the fp16-operand sum by {worst:.3g} past the fp32 bound"
+    assert np.array_equal(d_st.download(np.float16).reshape(2, ns), x16[:, n - ns:]), "fp16 state"

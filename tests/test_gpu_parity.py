@@ -160,7 +160,9 @@ def test_resample_vs_oracle(gpu_ctx, oracle, up, down, ntaps, ns, n):
 
 RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7, 101, 100, 700),
                   (5, 2, 151, 150, 400), (147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
-                  (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640)]
+                  (147, 1280, 101, 100, 12800), (7, 4, 151, 150, 4000), (64, 4, 101, 100, 640),
+                  # resample_lp item 1 would start inside the carried state (C*down < 152)
+                  (128, 4, 151, 150, 640)]
 # resample_lp with its loader wave (the default) and without, then resample_rs,
 # then the phase-major resample_pp
 RESAMPLE_KERNELS = {"lpw": {"SDR_RESAMPLE_LOADER": "1"}, "lp": {"SDR_RESAMPLE_LOADER": "0"},

@@ -246,3 +246,95 @@ def test_dropin_two_threads_at_once(harness, oracle, tmp_path):
             dm = oracle.frontend(D, I, Q, h, si, sq, pv)
             want += [dm, oracle.fir_block(dm, hb, sb)]
         assert_bits(got, np.concatenate(want), f"thread {t}")
+
+
+@pytest.mark.parametrize("D,T,ns", [(10, 101, 100), (10, 64, 63), (10, 101, 137)])
+def test_long_stream_segments_two_threads(built_lib, oracle, D, T, ns):
+    """SURVEY 8(e)'s one-long-stream split on the HIP path: a stream of four
+    cfg4 blocks (4 x 262,150 pairs) cut by sdrhip.shard.segment_plan into two
+    segments, each run by its own host thread and Context(0) -- the per-GPU
+    worker of bench.py --gpus N -- from a replicated halo only: the ns inputs
+    before its start as the FIR state, and its prev_I/Q recomputed by one
+    FIR+decimate call over [halo_lo, start).  The stitched demod and the last
+    segment's final state must equal ONE whole-stream call bit for bit, and
+    the oracle (state carry src/filter.cpp:139).  (T-1) % D != 0 at T = 64
+    (the generic kernel); T = 101 runs the fused fast path, ns = 137 a state
+    longer than T-1 and not a multiple of D."""
+    sdrhip = built_lib
+    from sdrhip.shard import segment_plan
+    from sdrhip.synth import fm_planar
+
+    N = 4 * 262150
+    nout = N // D
+    h = oracle.taps_lpf(2.4e6, 100e3, T, 1)
+    I, Q = fm_planar(N, seed=77 + T + ns)
+    rng = np.random.default_rng(ns)
+    s0 = rng.uniform(-0.7, 0.7, (2, ns)).astype(np.float32)  # the stream's carried state before it
+    p0 = np.array([0.3, -0.4], np.float32)
+
+    def before(x, st, p):
+        """the ns inputs before p (the carried state before the stream start)"""
+        return np.concatenate([st, x[:p]])[p:p + ns].copy()
+
+    segs = segment_plan(N, D, T, ns, 2)
+    res, errors = {}, []
+
+    def worker(seg):
+        try:
+            with sdrhip.Context(0) as ctx:
+                A = sdrhip.DeviceArray
+                d_h = A.from_numpy(ctx, h)
+                prev = p0.copy()
+                if seg.start:
+                    # prev_* = the decimated I/Q just before the segment, from the halo
+                    # [read_lo, start) only: I and Q as the two streams of one call
+                    lo, hl = seg.read_lo, seg.halo_lo
+                    xs = np.stack([I[hl:seg.start], Q[hl:seg.start]])
+                    st = np.stack([before(I, s0[0], hl), before(Q, s0[1], hl)])
+                    assert hl - ns >= lo or lo == 0
+                    nh = seg.start - hl
+                    d_x, d_st = A.from_numpy(ctx, xs), A.from_numpy(ctx, st)
+                    d_y = A(ctx, 2 * (nh // D) * 4)
+                    ctx.fir_decim_dev(D, d_x, nh, 2, nh, d_h, T, d_st, ns, d_y, nh // D)
+                    ctx.synchronize()
+                    prev = d_y.download().reshape(2, nh // D)[:, -1].copy()
+                si, sq = before(I, s0[0], seg.start), before(Q, s0[1], seg.start)
+                n = seg.length
+                d_I, d_Q = A.from_numpy(ctx, I[seg.start:seg.stop]), A.from_numpy(ctx, Q[seg.start:seg.stop])
+                d_si, d_sq = A.from_numpy(ctx, si), A.from_numpy(ctx, sq)
+                d_pi, d_pq = A.from_numpy(ctx, prev[:1]), A.from_numpy(ctx, prev[1:])
+                d_out = A(ctx, (n // D) * 4)
+                ctx.frontend_dev(D, d_I, d_Q, n, 1, n, d_h, T, d_si, d_sq, ns, d_pi, d_pq, d_out, n // D)
+                ctx.synchronize()
+                res[seg.rank] = (d_out.download(), d_si.download(), d_sq.download(),
+                                 np.concatenate([d_pi.download(), d_pq.download()]))
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append(f"segment {seg.rank}: {e!r}")
+
+    threads = [threading.Thread(target=worker, args=(s,)) for s in segs]
+    for t_ in threads:
+        t_.start()
+    for t_ in threads:
+        t_.join(timeout=100)
+    assert not any(t_.is_alive() for t_ in threads), "worker thread hung"
+    assert not errors, errors
+    got = np.concatenate([res[r][0] for r in range(2)])
+    assert got.shape == (nout,)
+    # one whole-stream call on the device
+    with sdrhip.Context(0) as ctx:
+        A = sdrhip.DeviceArray
+        d_I, d_Q, d_h = A.from_numpy(ctx, I), A.from_numpy(ctx, Q), A.from_numpy(ctx, h)
+        d_si, d_sq = A.from_numpy(ctx, s0[0]), A.from_numpy(ctx, s0[1])
+        d_pi, d_pq = A.from_numpy(ctx, p0[:1]), A.from_numpy(ctx, p0[1:])
+        d_out = A(ctx, nout * 4)
+        ctx.frontend_dev(D, d_I, d_Q, N, 1, N, d_h, T, d_si, d_sq, ns, d_pi, d_pq, d_out, nout)
+        ctx.synchronize()
+        whole = d_out.download()
+        wstate = (d_si.download(), d_sq.download(), np.concatenate([d_pi.download(), d_pq.download()]))
+    assert_bits(got, whole, "two stitched segments vs one whole-stream call")
+    for a, b, what in zip(res[1][1:], wstate, ("state_i", "state_q", "prev")):
+        assert_bits(a, b, f"last segment's final {what} vs the whole call")
+    si, sq, pv = s0[0].copy(), s0[1].copy(), p0.copy()
+    want = oracle.frontend(D, I, Q, h, si, sq, pv)
+    assert_bits(got, want, "stitched segments vs the oracle")
+    assert_bits(res[1][3], pv, "prev vs the oracle")
