@@ -41,6 +41,10 @@ struct LongArgs {
   int img;    // LDS floats per workgroup image
 };
 
+// VTAP = 1: the taps are staged in LDS behind the image and each pass's 32
+// are read into VGPRs by 8 wave-uniform (broadcast) ds_read_b128, so the
+// multiplies take no SGPR operand; VTAP = 0: SGPR taps (SDR_LONG_VTAP=0).
+template <int VTAP>
 __global__ __launch_bounds__(64 * kLongNW) void fir_long(LongArgs a) {
   extern __shared__ __attribute__((aligned(16))) float img[];
   constexpr int R = kLongR, KP = kLongKP, NTH = 64 * kLongNW;
@@ -72,6 +76,11 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long(LongArgs a) {
     }
     *reinterpret_cast<float4*>(img + 4 * c) = v;
   }
+  float* hl = img + a.img;  // the taps behind the image (a.img is a multiple of 4)
+  if constexpr (VTAP) {
+    for (int c = tid; c < (a.ntaps >> 2); c += NTH)
+      *reinterpret_cast<float4*>(hl + 4 * c) = *reinterpret_cast<const float4*>(a.h + 4 * c);
+  }
   __syncthreads();
 
   // ---- passes.  Lane window: output r of this lane sits at image index
@@ -87,10 +96,21 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long(LongArgs a) {
   constexpr int NC = (KP + R - 1) / 4 + 1;  // chunks per pass (relative indices 1 .. KP+R-1)
   for (int P = 0; P < npass; ++P) {
     float hs[KP];
+    if constexpr (VTAP) {
 #pragma unroll
-    for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
+      for (int i = 0; i < KP; i += 4) {
+        const float4 t = *reinterpret_cast<const float4*>(hl + P * KP + i);
+        hs[i] = t.x;
+        hs[i + 1] = t.y;
+        hs[i + 2] = t.z;
+        hs[i + 3] = t.w;
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
+      for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
+#pragma unroll
+      for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
+    }
     const float* base = img + lb + a.halo - KP * (P + 1);  // relative index 0, 16-B aligned
     float4 q = *reinterpret_cast<const float4*>(base + 4 * (NC - 1));
 #pragma unroll
@@ -158,7 +178,13 @@ hipError_t launch_fir_long(const FirLaunch& f, const float* h, hipStream_t st) {
   a.img = a.halo + OUT_WG + 4;
   const long long blocks = (long long)a.tiles_per_stream * f.nstreams;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fir_long, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * sizeof(float), st, a);
+  // SDR_LONG_VTAP=0: SGPR taps (A/B; read per launch).  The tap copy needs
+  // 16-B aligned taps (ntaps is a multiple of 32).
+  if (env_int("SDR_LONG_VTAP", 1) != 0 && (reinterpret_cast<uintptr_t>(h) & 15) == 0)
+    hipLaunchKernelGGL(fir_long<1>, dim3((unsigned)blocks), dim3(64 * kLongNW),
+                       (size_t)(a.img + f.ntaps) * sizeof(float), st, a);
+  else
+    hipLaunchKernelGGL(fir_long<0>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * sizeof(float), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || f.ns <= 0) return e;
   hipLaunchKernelGGL(long_commit, dim3((f.ns + kWG - 1) / kWG, (unsigned)f.nstreams), dim3(kWG), 0, st, f.x0, f.n,
@@ -197,6 +223,12 @@ struct LongHArgs {
   int img;    // image halves (multiple of 8)
 };
 
+// VTAP = 1 (the default): the tap-pair table is staged in LDS after the
+// image and each pass's 32 pairs are read into VGPRs by 8 wave-uniform
+// (broadcast) ds_read_b128, so every v_dot2_f32_f16 has VGPR operands only.
+// VTAP = 0: the pairs are SGPR operands of the dot2 (one scalar batch per
+// pass), which halves the dot2 issue rate.
+template <int VTAP>
 __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t imgw[];  // image as packed pairs
   constexpr int R = kLongRH, NTH = 64 * kLongNW, KP = 32;  // KP tap pairs (d values) per pass
@@ -223,6 +255,13 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
       }
     }
   }
+  // the tap-pair table behind the image (a.img halves = a.img / 2 words)
+  uint32_t* hpl = imgw + (a.img >> 1);
+  const int npairs = (a.ntaps + 1 + 31) / 32 * 32;
+  if constexpr (VTAP) {
+    for (int c = tid; c < (npairs >> 2); c += NTH)
+      *reinterpret_cast<uint4*>(hpl + 4 * c) = *reinterpret_cast<const uint4*>(a.hp2 + 4 * c);
+  }
   __syncthreads();
 
   // output r of this lane: image half index i_r = I0 + r, I0 = lb + halo
@@ -236,10 +275,21 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
   const int npass = (a.ntaps + 1 + KP - 1) / KP;  // d = 0..T
   for (int P = 0; P < npass; ++P) {
     uint32_t hs[KP];
+    if constexpr (VTAP) {
 #pragma unroll
-    for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
+      for (int i = 0; i < KP; i += 4) {
+        const uint4 t = *reinterpret_cast<const uint4*>(hpl + P * KP + i);
+        hs[i] = t.x;
+        hs[i + 1] = t.y;
+        hs[i + 2] = t.z;
+        hs[i + 3] = t.w;
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
+      for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
+#pragma unroll
+      for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
+    }
     // pair W for (r, d): 2W = I0 + r - d, d = KP*P + dd.  Word index
     // W = I0/2 - KP*P/2 + (r - dd)/2 ranges over base + [-(KP/2), 1].
     const int wbase = (I0 >> 1) - (KP / 2) * P - (KP / 2);  // word of relative index 0
@@ -330,7 +380,12 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
   a.img = a.halo + OUT_WG + 8;
   const long long blocks = (long long)a.tiles_per_stream * nstreams;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fir_long_h, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2, st, a);
+  // SDR_F16_VTAP=0: SGPR tap pairs (A/B; read per launch)
+  if (env_int("SDR_F16_VTAP", 1) != 0)
+    hipLaunchKernelGGL(fir_long_h<1>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2 + (size_t)len * 4,
+                       st, a);
+  else
+    hipLaunchKernelGGL(fir_long_h<0>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2, st, a);
   e = hipGetLastError();
   if (e != hipSuccess || ns <= 0) return e;
   hipLaunchKernelGGL(long_commit_h, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st,
