@@ -223,11 +223,11 @@ struct LongHArgs {
   int img;    // image halves (multiple of 8)
 };
 
-// VTAP = 1 (the default): the tap-pair table is staged in LDS after the
+// VTAP = 1 (A/B, SDR_F16_VTAP=1): the tap-pair table is staged in LDS after the
 // image and each pass's 32 pairs are read into VGPRs by 8 wave-uniform
 // (broadcast) ds_read_b128, so every v_dot2_f32_f16 has VGPR operands only.
 // VTAP = 0: the pairs are SGPR operands of the dot2 (one scalar batch per
-// pass), which halves the dot2 issue rate.
+// pass), which halves the dot2 issue rate -- still the faster.
 template <int VTAP>
 __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t imgw[];  // image as packed pairs
@@ -380,8 +380,11 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
   a.img = a.halo + OUT_WG + 8;
   const long long blocks = (long long)a.tiles_per_stream * nstreams;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  // SDR_F16_VTAP=0: SGPR tap pairs (A/B; read per launch)
-  if (env_int("SDR_F16_VTAP", 1) != 0)
+  // SDR_F16_VTAP=1: VGPR tap pairs from LDS (A/B; read per launch).  Not the
+  // default: 0.0544 vs 0.0425 ms on cfg5h (profiles/r04a/ab_vtap.txt) -- the
+  // 8 broadcast ds_read_b128 per pass cost 4 LDS cycles per wave each, which
+  // with the 10 input reads puts 16 waves per CU past the LDS array's rate.
+  if (env_int("SDR_F16_VTAP", 0) != 0)
     hipLaunchKernelGGL(fir_long_h<1>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2 + (size_t)len * 4,
                        st, a);
   else

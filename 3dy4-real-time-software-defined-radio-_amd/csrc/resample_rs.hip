@@ -377,7 +377,23 @@ __device__ __forceinline__ int lp_lane_code(int up, int down, int S, int base0, 
     codes[(g >> 2) * 64 + kB128Groups[g & 3][m]] = (item % up) | ((item / up) << 16);
   }
   __syncthreads();
-  return codes[t];
+  // A slot left empty still issues the scan's reads: as (0, 0) it would add a
+  // second address of one bank class to its lane group -- one extra LDS
+  // cycle on every ds_read_b128 of that group (the 448 - 441 empty slots at
+  // L = 147 sit in 7 of the 28 groups: ~23 % SQ_LDS_BANK_CONFLICT).  It
+  // shadows its group's first member instead (same address = a broadcast)
+  // and is flagged 0x8000 so it stores nothing.
+  int code = codes[t];
+  if (code < 0) {
+    const int l = t & 63, w = t >> 6;
+    for (int g4 = 0; g4 < 4; ++g4)
+      for (int m = 0; m < 16; ++m)
+        if (kB128Groups[g4][m] == l) {
+          const int twin = codes[w * 64 + kB128Groups[g4][0]];
+          if (twin >= 0) code = twin | 0x8000;
+        }
+  }
+  return code;
 }
 
 // One launch for both tables of resample_lp: blocks 0..G-2 write the shifted
@@ -457,7 +473,10 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
   for (int k = 0; k < K; ++k) {
     const int c = sub + a.S * k;
     act[k] = valid && c < ce;
-    const int cc = c < ce ? c : 0;
+    // an idle chain (ragged last item) reads a column of the same parity: the
+    // chunk's bank class is 8*column + const (mod 16, down/4 = 200 at cfg3),
+    // so its lane keeps its class and adds no conflict
+    const int cc = c < ce ? c : ((c & 1) < ce ? (c & 1) : 0);
     ptr[k] = (lds4*)(buf + 4 * (cc * (a.down >> 2) + ctop0 - (NC - 1)));
     asm volatile("" : "+v"(ptr[k]));  // keep the base in a VGPR: per-chunk offsets stay immediates
   }
@@ -537,8 +556,8 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   // the first item's DMA runs while this lane's item and taps are loaded
   stage(bufA, i0);
   const int code = loader ? -1 : a.lanes[threadIdx.x];
-  const bool valid = code >= 0;
-  const int phi = valid ? (code & 0xffff) : 0, sub = valid ? (code >> 16) : 0;
+  const bool valid = code >= 0 && !(code & 0x8000);  // 0x8000: an empty slot shadowing a twin
+  const int phi = code >= 0 ? (code & 0x7fff) : 0, sub = code >= 0 ? (code >> 16) : 0;
   const int q = (int)((long long)phi * a.down / a.up);
   const int A = (q - base0) & 3, ctop0 = (q - base0) >> 2;
   const int p = (int)((long long)phi * a.down % a.up);

@@ -44,7 +44,7 @@ if [ -n "${PMC:-}" ]; then
   for cfg in cfg2 ${PMC_CFGS:-}; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_${cfg}_$ctr" -o pmc \
-        -- python3 bench.py --config $cfg --steps 3 --warmup 1 --warm-seconds 0 --no-cpu-baseline --no-fma-variant --no-graph \
+        -- python3 bench.py --config $cfg --steps 3 --warmup 1 --warm-seconds 0 --no-cpu-baseline --no-fma-variant --no-graph --sustain-seconds 0 \
         > /dev/null 2>> "$OUT/prof.err"
       rc=$?; echo "pmc $cfg $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
     done

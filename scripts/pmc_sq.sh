@@ -13,7 +13,7 @@ while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$PWD/$OUT/p$i" -o pmc \
-     -- python3 bench.py --config $CFG --steps 3 --warmup 1 --warm-seconds 0 --no-cpu-baseline --no-fma-variant \
+     -- python3 bench.py --config $CFG --steps 3 --warmup 1 --warm-seconds 0 --no-cpu-baseline --no-fma-variant --sustain-seconds 0 \
         --no-graph > /dev/null 2>> "$OUT/err.log"
   rc=$?; echo "pass $i ($grp) rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done <<GROUPS

@@ -9,7 +9,7 @@ for rep in $(seq ${REPS:-2}); do
       lib=${arm%%:*}; envs=${arm#*:}
       e=""; [ "$envs" = default ] || e="${envs//,/ }"
       if [ "$lib" = tree ]; then unset SDRHIP_LIB; else export SDRHIP_LIB=$PWD/$lib; fi
-      r=$(env $e timeout -k 10 120 python bench.py --config $cfg --steps ${STEPS:-100} --warmup 3 --no-cpu-baseline --no-fma-variant 2>>gpurun_out/sweep.err |
+      r=$(env $e timeout -k 10 120 python bench.py --config $cfg --steps ${STEPS:-100} --warmup 3 --no-cpu-baseline --no-fma-variant --sustain-seconds 0 2>>gpurun_out/sweep.err |
           python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['ms_per_step'], d['roofline']['frac'])")
       rc=$?; echo "rep $rep $cfg $arm: $r"; [ $rc -eq 0 ] || exit $rc
     done
