@@ -458,7 +458,7 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
   }
 }
 
-template <int CMAX, int K, int LW>
+template <int CMAX, int K, int LW, int NOLDS = 0>
 __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, int it, const float (&tp)[(CMAX + 6) / 4 * 4],
                                            int phi, int sub, int A, int ctop0, bool valid) {
   constexpr int NC = (CMAX + 6) / 4;
@@ -492,7 +492,15 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
     // the next chunk's reads go out first; this chunk's were issued one chunk ago
     if (cc + 1 < NC) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) nxt[k] = ptr[k][NC - 2 - cc];
+      for (int k = 0; k < K; ++k) {
+        if constexpr (NOLDS) {
+          // timing ablation (SDR_ABLATE=4): the scan without its LDS reads
+          nxt[k] = cur[k];
+          asm volatile("" : "+v"(nxt[k]));
+        } else {
+          nxt[k] = ptr[k][NC - 2 - cc];
+        }
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -532,7 +540,7 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
 // the seven compute waves only scan: the DMA issue -- 3-4 k cycles of each
 // compute wave's item time -- leaves their instruction
 // streams; its registers come free with the 2-waves-per-SIMD allocation.
-template <int CMAX, int K, int LW>
+template <int CMAX, int K, int LW, int NOLDS = 0>
 __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   __shared__ __attribute__((aligned(16))) float bufA[kLpBuf];
   __shared__ __attribute__((aligned(16))) float bufB[kLpBuf];
@@ -597,9 +605,9 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     if (it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
     if (a.ablate != 2 && !loader) {
       if (odd)
-        lp_compute<CMAX, K, LW>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
+        lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
       else
-        lp_compute<CMAX, K, LW>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
+        lp_compute<CMAX, K, LW, NOLDS>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
     }
     if (!LW && commit && (int)threadIdx.x < a.ns) {
       dma_drain();
@@ -722,7 +730,11 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       }
       const int grid = b.nitems < ncu ? b.nitems : ncu;
       const dim3 g((unsigned)grid);
-      if (lp_loader()) {
+      if (ablate == 4 && cmax == 151 && K == 7) {
+        // timing ablation: no staging and no LDS reads in the scan
+        b.ablate = 1;
+        hipLaunchKernelGGL((resample_lp<151, 7, 1, 1>), g, dim3(kLpSlots + 64), 0, st, b);
+      } else if (lp_loader()) {
         const dim3 blk(kLpSlots + 64);
         if (cmax == 151) {
           if (K == 4)
