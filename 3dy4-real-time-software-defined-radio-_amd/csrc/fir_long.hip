@@ -329,6 +329,134 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
   }
 }
 
+// ---- MFMA form (the default for T % 8 == 0): the FIR as a Toeplitz GEMM on
+// v_mfma_f32_32x32x16_f16.  A 32x32 tile of outputs m = m0 + i + 32 j
+// (i = row, j = column: 32 blocks of 32 consecutive outputs) is
+//   D[i][j] = sum_t A[i][t] B[t][j],  A[i][t] = h[i + T - t]  (0 outside [0, T)),
+//                                     B[t][j] = x~[m0 + 32 j + t - T],
+// t = 0 .. KD-1, KD = roundup96(T + 31): 66 MFMAs per 1,024 outputs at T =
+// 1024 (3 % of them on the band's zero corners).  B's fragment (lane: column
+// j = l & 31, k-half h = l >> 5) is 8 consecutive inputs -- one 16-B LDS read
+// from the staged input image (a 16-B pad per 64 B row keeps the 32 columns'
+// reads, 64 B apart, on distinct banks); A's fragment is 8 consecutive
+// reversed taps starting at 16 s + 8 h - i - 1, read 16-B aligned from one of
+// eight copies of the reversed f16 taps, copy q shifted by q halves.
+// Same operands as the dot2 kernel (fp16 x, state and taps), fp32
+// accumulation inside the MFMA: the same tolerance contract.
+constexpr int kMfNT = 2;                      // 1,024-output tiles per wave
+constexpr int kMfWaves = 4;                   // one wave per SIMD
+constexpr int kMfOut = 1024 * kMfNT * kMfWaves;  // outputs per workgroup
+
+struct MfArgs {
+  const _Float16* x;
+  long long n, x_stride;  // halves
+  const float* h;
+  int ntaps, kd, lc;      // taps, K extent (multiple of 16), halves per tap copy
+  const _Float16* state;
+  int ns;
+  float* y;
+  long long y_stride;
+  int wg_per_stream;
+  int span;               // staged input halves per workgroup (kMfOut + kd - 32)
+};
+
+__host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
+
+__global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
+  typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+  typedef float f16x __attribute__((ext_vector_type(16)));
+  extern __shared__ __attribute__((aligned(16))) _Float16 mf_lds[];
+  _Float16* img = mf_lds;                              // padded input image
+  _Float16* hcp = mf_lds + mf_pad(a.span) + 8;         // 8 tap copies, a.lc halves each
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int s = blockIdx.x / a.wg_per_stream;
+  const long long m0 = (long long)(blockIdx.x - s * a.wg_per_stream) * kMfOut;
+  const long long pb = m0 - a.ntaps;                   // stream position of image element 0 (multiple of 8)
+  const _Float16* xs = a.x + (long long)s * a.x_stride;
+  const _Float16* st = a.state + (long long)s * a.ns;
+  // ---- stage the input image: 16-B chunks, element-wise at the block edges
+  for (int c = tid; c < (a.span >> 3); c += 64 * kMfWaves) {
+    const long long p = pb + 8LL * c;
+    _Float16* d = img + mf_pad(8 * c);
+    if (p >= 0 && p + 8 <= a.n) {
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(xs + p);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const long long q = p + r;
+        d[r] = q >= 0 ? (q < a.n ? xs[q] : (_Float16)0) : (q >= -a.ns ? st[a.ns + q] : (_Float16)0);
+      }
+    }
+  }
+  // ---- the tap copies: copy q, element w = hr[w + q - 32], hr[v] = h[T-1-v]
+  for (int e = tid; e < 8 * a.lc; e += 64 * kMfWaves) {
+    const int q = e / a.lc, w = e - q * a.lc;
+    const int v = w + q - 32;
+    hcp[e] = (v >= 0 && v < a.ntaps) ? (_Float16)a.h[a.ntaps - 1 - v] : (_Float16)0;
+  }
+  __syncthreads();
+  const int i = lane & 31, hh = lane >> 5;
+  const int q = 7 - (i & 7);                            // (-i-1) mod 8
+  const _Float16* arow = hcp + q * a.lc + (8 * hh - i - 1 + 32 - q);  // + 16 s: A fragment of step s
+  const int tb0 = wave * kMfNT * 1024;                  // this wave's first tile, relative to m0
+  f16x acc[kMfNT];
+#pragma unroll
+  for (int t = 0; t < kMfNT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+  // G steps per group; the next group's 3 G fragments are read while this
+  // group's 2 G MFMAs run (kd is a multiple of 32 G: an even group count)
+  constexpr int G = 3;
+  const int ngrp = a.kd / (16 * G);
+  half8 av[G], bv[G][kMfNT];
+  auto fetch = [&](int g0, half8 (&aa)[G], half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int sidx = g0 * G + u;
+      aa[u] = *reinterpret_cast<const half8*>(arow + 16 * sidx);
+#pragma unroll
+      for (int t = 0; t < kMfNT; ++t) {
+        const int p = tb0 + t * 1024 + 32 * i + 16 * sidx + 8 * hh;  // image index of B's fragment
+        bb[u][t] = *reinterpret_cast<const half8*>(img + mf_pad(p));
+      }
+    }
+  };
+  auto mfmas = [&](const half8 (&aa)[G], const half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+      for (int t = 0; t < kMfNT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[u], bb[u][t], acc[t], 0, 0, 0);
+  };
+  // two register sets in ping-pong (ngrp is even): no copies between groups
+  half8 an[G], bn[G][kMfNT];
+  fetch(0, av, bv);
+  for (int g = 0; g < ngrp; g += 2) {
+    fetch(g + 1, an, bn);
+    mfmas(av, bv);
+    if (g + 2 < ngrp) fetch(g + 2, av, bv);
+    mfmas(an, bn);
+  }
+  // ---- outputs: lane (column j = i, half hh) holds rows (r & 3) + 8 (r >> 2) + 4 hh
+  float* ys = a.y + (long long)s * a.y_stride;
+#pragma unroll
+  for (int t = 0; t < kMfNT; ++t) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const long long m = m0 + tb0 + t * 1024 + 32 * i + 8 * g + 4 * hh;
+      const float4 v = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+      if (m + 4 <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
+        *reinterpret_cast<float4*>(ys + m) = v;
+      } else {
+        const float w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (m + r < a.n) ys[m + r] = w[r];
+      }
+    }
+  }
+}
+
 // hp2[d] = (half(h[d]), half(h[d-1])) for d = 0..T, zero past both ends and
 // up to the padded length.
 __global__ __launch_bounds__(kWG) void build_pairs_h(const float* __restrict__ h, int ntaps, int len, uint32_t* hp2) {
@@ -360,6 +488,34 @@ size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32)
 hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
                              void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
                              hipStream_t st) {
+  // the MFMA form: T % 8 == 0 keeps the staged image's 16-B chunks aligned
+  // (x rows are 16-B aligned, checked by the caller); SDR_F16_MFMA=0 selects
+  // the dot2 kernel below (A/B, tests)
+  if (ntaps % 8 == 0 && env_int("SDR_F16_MFMA", 1) != 0) {
+    MfArgs a;
+    a.x = static_cast<const _Float16*>(x);
+    a.n = n;
+    a.x_stride = x_stride;
+    a.h = h;
+    a.ntaps = ntaps;
+    a.kd = (ntaps + 31 + 95) / 96 * 96;  // an even number of 3-step groups (zero taps past the band)
+    a.lc = (a.kd + 40 + 7) / 8 * 8;
+    a.state = static_cast<const _Float16*>(state);
+    a.ns = ns;
+    a.y = y;
+    a.y_stride = y_stride;
+    a.wg_per_stream = (int)((n + kMfOut - 1) / kMfOut);
+    a.span = kMfOut + a.kd - 32;
+    const size_t lds = ((size_t)mf_pad(a.span) + 8 + 8 * (size_t)a.lc) * sizeof(_Float16);
+    const long long blocks = (long long)a.wg_per_stream * nstreams;
+    if (blocks > 0x7fffffffLL || lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fir_long_mfma, dim3((unsigned)blocks), dim3(64 * kMfWaves), lds, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || ns <= 0) return e;
+    hipLaunchKernelGGL(long_commit_h, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st,
+                       static_cast<const _Float16*>(x), n, x_stride, static_cast<_Float16*>(state), ns);
+    return hipGetLastError();
+  }
   const int len = (int)fir_long_h_pairs(ntaps);
   hipLaunchKernelGGL(build_pairs_h, dim3((len + kWG - 1) / kWG), dim3(kWG), 0, st, h, ntaps, len, scratch_pairs);
   hipError_t e = hipGetLastError();

@@ -10,3 +10,7 @@ rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit 
 ARMS="SDR_FIR_VTAP_U8=0 SDR_FIR_VTAP_U8=1" CFGS="cfg2u8 mono0" REPS=2 bash scripts/sweep_env.sh || exit 1
 ARMS="SDR_FIR_VTAP=0 SDR_FIR_VTAP=1" CFGS="cfg2" REPS=2 bash scripts/sweep_env.sh || exit 1
 ARMS="SDR_ABLATE=0 SDR_ABLATE=1 SDR_ABLATE=2 SDR_ABLATE=4" CFGS="cfg3" REPS=2 bash scripts/sweep_env.sh || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q -p no:cacheprovider \
+  -rf --timeout 300 --timeout-method thread -k "f16" > "$OUT/pytest_f16.log" 2>&1
+rc=$?; tail -3 "$OUT/pytest_f16.log"; [ $rc -eq 0 ] || { echo "pytest f16 rc=$rc"; exit $rc; }
+ARMS="SDR_F16_MFMA=1 SDR_F16_MFMA=0" CFGS="cfg5h" REPS=2 bash scripts/sweep_env.sh || exit 1

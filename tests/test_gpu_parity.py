@@ -274,12 +274,16 @@ def test_resample_many_streams(gpu_ctx, oracle, built_lib, up, down, cnt, nstrea
         assert_bits(d_st.download().reshape(nstreams, ns), states, f"state block {blk}")
 
 
-@pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000)])
-def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, ntaps, n):
-    """BASELINE config 5's fp16 arm (fp16 storage, fp32 dot2 accumulation):
-    within 2^-9 * sum|h| * max|x| of the exact fp32 reference, and within
-    fp32 accumulation error of the exact sum over the fp16-rounded operands.
-    The carried fp16 state is the last ns inputs, exactly."""
+@pytest.mark.parametrize("kernel", ["mfma", "dot2"])
+@pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000), (256, 8193), (8, 700)])
+def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, monkeypatch, ntaps, n, kernel):
+    """BASELINE config 5's fp16 arm (fp16 storage, fp32 accumulation -- the
+    Toeplitz-GEMM v_mfma_f32_32x32x16_f16 kernel for T % 8 == 0, else / under
+    SDR_F16_MFMA=0 the v_dot2_f32_f16 kernel): within 2^-9 * sum|h| * max|x|
+    of the exact fp32 reference, and within fp32 accumulation error of the
+    exact sum over the fp16-rounded operands.  The carried fp16 state is the
+    last ns inputs, exactly."""
+    monkeypatch.setenv("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(ntaps + n)
     h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
