@@ -4,6 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r04c; mkdir -p $OUT
+timeout -k 10 120 ./tools/ubench_ldsmix > "$OUT/ubench_ldsmix.txt" 2>&1; rc=$?; cat "$OUT/ubench_ldsmix.txt"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q -p no:cacheprovider \
   -rf --timeout 300 --timeout-method thread -k "frontend or cfg2" > "$OUT/pytest.log" 2>&1
 rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
