@@ -411,6 +411,14 @@ int sdr_event_synchronize(sdr_ctx* c, sdr_event* ev) {
   return SDR_OK;
 }
 
+int sdr_ctx_wait_event(sdr_ctx* c, sdr_event* ev) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!ev) return fail(c, SDR_EINVAL, "null event");
+  SDR_HIP(c, hipStreamWaitEvent(c->cur, ev->ev, 0));
+  return SDR_OK;
+}
+
 int sdr_event_destroy(sdr_ctx* c, sdr_event* ev) {
   int rc = enter(c);
   if (rc) return rc;
@@ -958,6 +966,118 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs
     return rc;
   // :131-132 + 304-314: L/R, interleave, s16
   return sdr_stereo_pcm_dev(c, mono, slp, na, nstreams, astride, pcm, pcm_stride);
+}
+
+// ---------------------------------------------- stereo path in two stages --
+// The same calls as sdr_stereo_pcm_u8_dev, cut where the PLL recurrence
+// starts, with one block's intermediates in a caller-owned work object so a
+// block's front stage can run on one context's stream while the previous
+// block's back stage (the recurrence) runs on another's (host/sdr_project.cpp).
+// The stages touch disjoint state: front = RF front end, delay, mono
+// resampler, pilot and stereo band-pass states; back = PLL and the stereo
+// resampler state.
+struct sdr_stereo_work {
+  int D = 0, up = 0, down = 0, nstreams = 0;
+  long long npairs = 0, nd = 0, na = 0, dstride = 0, astride = 0, pstride = 0;
+  void* mem = nullptr;
+  float *demod = nullptr, *delayed = nullptr, *mono = nullptr, *pilot = nullptr, *sband = nullptr, *slp = nullptr,
+        *args = nullptr, *mixed = nullptr;
+  uint8_t* guard = nullptr;
+};
+
+int sdr_stereo_work_create(sdr_ctx* c, int D, long long npairs, int up, int down, int nstreams,
+                           sdr_stereo_work** out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!out) return fail(c, SDR_EINVAL, "null work");
+  *out = nullptr;
+  if (D < 1 || npairs <= 0 || npairs % D || nstreams < 1 || up < 1 || down < 1)
+    return fail(c, SDR_EINVAL, "bad stereo work shape");
+  auto* w = new sdr_stereo_work;
+  w->D = D, w->up = up, w->down = down, w->nstreams = nstreams, w->npairs = npairs;
+  w->nd = npairs / D;
+  w->na = sdr_resample_out_len(up, down, w->nd);
+  if (w->na <= 0) {
+    delete w;
+    return fail(c, SDR_EINVAL, "empty audio block");
+  }
+  w->dstride = (w->nd + 3) / 4 * 4, w->astride = (w->na + 3) / 4 * 4, w->pstride = (w->nd + 1 + 3) / 4 * 4;
+  const size_t d = (size_t)nstreams * w->dstride, a = (size_t)nstreams * w->astride,
+               p = (size_t)nstreams * w->pstride;
+  const size_t g = (sdr::pll_guard_bytes(w->nd, nstreams) + 15) / 16 * 16;
+  const size_t floats = 5 * d + 2 * a + p;
+  hipError_t e = hipMalloc(&w->mem, floats * sizeof(float) + g);
+  if (e != hipSuccess) {
+    delete w;
+    return fail(c, SDR_ENOMEM, "stereo work buffers");
+  }
+  float* f = static_cast<float*>(w->mem);
+  w->demod = f, f += d;
+  w->delayed = f, f += d;
+  w->pilot = f, f += d;
+  w->sband = f, f += d;
+  w->mixed = f, f += d;
+  w->mono = f, f += a;
+  w->slp = f, f += a;
+  w->args = f, f += p;
+  w->guard = reinterpret_cast<uint8_t*>(f);
+  *out = w;
+  return SDR_OK;
+}
+
+int sdr_stereo_work_destroy(sdr_ctx* c, sdr_stereo_work* w) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (w) {
+    (void)hipStreamSynchronize(c->cur);  // the caller's last use is on this context's stream
+    (void)hipFree(w->mem);
+    delete w;
+  }
+  return SDR_OK;
+}
+
+// front end (src/project.cpp:72-93), delay + mono resampler (:114-116),
+// stereo band-pass (:121), pilot band-pass (:120)
+int sdr_stereo_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, const sdr_stereo_taps* taps,
+                            sdr_stereo_state* st, sdr_stereo_work* w) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!taps || !st || !w) return fail(c, SDR_EINVAL, "null taps / state / work");
+  const int n = w->nstreams;
+  if ((rc = sdr_frontend_u8_dev(c, w->D, iq, w->npairs, n, iq_stride, taps->h_rf, taps->rf_taps, st->state_i,
+                                st->state_q, st->ns_rf, st->prev_i, st->prev_q, w->demod, w->dstride)))
+    return rc;
+  if ((rc = sdr_delay_f32_dev(c, w->demod, w->nd, n, w->dstride, st->delay_state, st->ns_delay, w->delayed,
+                              w->dstride)))
+    return rc;
+  if ((rc = sdr_resample_f32_dev(c, w->up, w->down, w->delayed, w->nd, n, w->dstride, taps->h_audio,
+                                 taps->audio_taps, st->state_audio, st->ns_audio, w->mono, w->astride)))
+    return rc;
+  if ((rc = sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_stereo, taps->bpf_taps,
+                                  st->stereo_state, st->ns_bpf, w->sband, w->dstride)))
+    return rc;
+  return sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_pilot, taps->bpf_taps, st->pilot_state,
+                               st->ns_bpf, w->pilot, w->dstride);
+}
+
+// PLL recurrence (:123-126), NCO x stereo band (:127), stereo resampler
+// (:129), L/R + interleave + s16 (:131-132, 304-314)
+int sdr_stereo_back_dev(sdr_ctx* c, float audio_fs, const sdr_stereo_taps* taps, sdr_stereo_state* st,
+                        sdr_stereo_work* w, int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!taps || !st || !w || !pcm) return fail(c, SDR_EINVAL, "null taps / state / work / pcm");
+  const int n = w->nstreams;
+  if (n > 1 && pcm_stride < 2 * w->na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
+  hipError_t e = sdr::launch_pll_recurrence(w->pilot, w->nd, n, w->dstride, 19e3f, audio_fs, 2.0f, 0.0f, 0.01f,
+                                            st->pll, w->args, w->pstride, c->cur, w->guard);
+  if (e != hipSuccess) return hip_fail(c, e, "pll launch");
+  e = sdr::launch_nco(w->args, w->pstride, w->nd, n, 2.0f, 0.0f, w->sband, w->dstride, w->mixed, w->dstride, c->cur);
+  if (e != hipSuccess) return hip_fail(c, e, "nco launch");
+  if ((rc = sdr_resample_f32_dev(c, w->up, w->down, w->mixed, w->nd, n, w->dstride, taps->h_audio, taps->audio_taps,
+                                 st->stereo_lp_state, st->ns_audio, w->slp, w->astride)))
+    return rc;
+  return sdr_stereo_pcm_dev(c, w->mono, w->slp, w->na, n, w->astride, pcm, pcm_stride);
 }
 
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

@@ -199,6 +199,50 @@ int main(int argc, char* argv[]) {
   const bool use_graph = !(nog && std::atoi(nog) != 0);
   sdr_graph* graph[2] = {nullptr, nullptr};
 
+  // Stereo: the block is cut where the PLL recurrence starts (sdr_stereo_front_u8_dev /
+  // sdr_stereo_back_dev, disjoint state).  The front stage runs on g_ctx's stream, the
+  // back stage on a second context's, so block b+1's copy-in, front end and band-pass
+  // filters overlap block b's recurrence -- the one-lane PLL is most of a stereo block
+  // (DESIGN.md 4.7).  Each ring slot has its own work object; front(b) waits for
+  // back(b-2) (the slot's previous user), back(b) for front(b).  SDR_PROJECT_SPLIT=0
+  // runs the whole block as one call instead.
+  const char* spl = std::getenv("SDR_PROJECT_SPLIT");
+  const bool split = !mono && !(spl && std::atoi(spl) == 0);
+  sdr_ctx* g_back = nullptr;
+  sdr_stereo_work* work[2] = {nullptr, nullptr};
+  sdr_event* front_done[2] = {nullptr, nullptr};
+  sdr_graph* graph_back[2] = {nullptr, nullptr};
+  if (split) {
+    check(sdr_ctx_create(devenv ? std::atoi(devenv) : 0, &g_back), "ctx_create");
+    for (int i = 0; i < 2; ++i) {
+      check(sdr_stereo_work_create(g_ctx, rf_decim, npairs, audio_up, audio_decim, 1, &work[i]), "stereo_work_create");
+      check(sdr_event_create(g_ctx, &front_done[i]), "event_create");
+    }
+  }
+  auto enqueue_front = [&](int k) {
+    check(sdr_copy_h2d_async(g_ctx, d_in[k], h_in[k], block_size), "copy_h2d_async");
+    check(sdr_stereo_front_u8_dev(g_ctx, static_cast<const uint8_t*>(d_in[k]), 2 * npairs, &taps, &st, work[k]),
+          "stereo_front_u8_dev");
+  };
+  auto enqueue_back = [&](int k) {
+    check(sdr_stereo_back_dev(g_back, audio_Fs, &taps, &st, work[k], static_cast<int16_t*>(d_out[k]), pcm_len),
+          "stereo_back_dev");
+    check(sdr_copy_d2h_async(g_back, h_out[k], d_out[k], pcm_len * sizeof(int16_t)), "copy_d2h_async");
+  };
+  // run f on ctx directly (block 0 sizes the scratch) or as slot k's recorded graph
+  auto run = [&](sdr_ctx* ctx, sdr_graph** g, bool direct, auto&& f) {
+    if (direct) {
+      f();
+      return;
+    }
+    if (!*g) {
+      check(sdr_graph_begin(ctx), "graph_begin");
+      f();
+      check(sdr_graph_end(ctx, g), "graph_end");
+    }
+    check(sdr_graph_launch(ctx, *g), "graph_launch");
+  };
+
   auto flush = [&](unsigned b) {  // wait for block b and write its PCM (src/project.cpp:315)
     check(sdr_event_synchronize(g_ctx, done[b & 1]), "event_synchronize");
     std::fwrite(h_out[b & 1], sizeof(int16_t), pcm_len, stdout);
@@ -214,17 +258,20 @@ int main(int argc, char* argv[]) {
       std::cerr << "End of input stream reached" << std::endl;
       std::exit(1);  // as the reference (src/project.cpp:294-297)
     }
-    if (block_id == 0 || !use_graph) {
-      enqueue(k);  // the first block sizes the library's scratch (no allocation may happen inside a capture)
+    // the first block sizes the library's scratch (no allocation may happen
+    // inside a capture); then each ring slot's sequence is recorded once and replayed
+    const bool direct = block_id == 0 || !use_graph;
+    if (split) {
+      if (block_id >= 2) check(sdr_ctx_wait_event(g_ctx, done[k]), "wait_event");  // back(b-2) released work[k]
+      run(g_ctx, &graph[k], direct, [&] { enqueue_front(k); });
+      check(sdr_event_record(g_ctx, front_done[k]), "event_record");
+      check(sdr_ctx_wait_event(g_back, front_done[k]), "wait_event");
+      run(g_back, &graph_back[k], direct, [&] { enqueue_back(k); });
+      check(sdr_event_record(g_back, done[k]), "event_record");
     } else {
-      if (!graph[k]) {  // record slot k's sequence once, then replay it for every block in that slot
-        check(sdr_graph_begin(g_ctx), "graph_begin");
-        enqueue(k);
-        check(sdr_graph_end(g_ctx, &graph[k]), "graph_end");
-      }
-      check(sdr_graph_launch(g_ctx, graph[k]), "graph_launch");
+      run(g_ctx, &graph[k], direct, [&] { enqueue(k); });
+      check(sdr_event_record(g_ctx, done[k]), "event_record");
     }
-    check(sdr_event_record(g_ctx, done[k]), "event_record");
     // block_id - 1's PCM goes out while the device runs block_id and the
     // next read waits on stdin
     if (block_id > 0) flush(block_id - 1);

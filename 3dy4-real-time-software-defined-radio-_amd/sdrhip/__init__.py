@@ -70,6 +70,7 @@ _SIGS = {
     "sdr_event_record": [_vp, _vp],
     "sdr_event_synchronize": [_vp, _vp],
     "sdr_event_destroy": [_vp, _vp],
+    "sdr_ctx_wait_event": [_vp, _vp],
     "sdr_graph_begin": [_vp],
     "sdr_graph_end": [_vp, C.POINTER(_vp)],
     "sdr_graph_launch": [_vp, _vp],
@@ -102,6 +103,10 @@ _SIGS = {
                        _ll, _vp, _ll],
     "sdr_stereo_pcm_dev": [_vp, _vp, _vp, _ll, _i, _ll, _vp, _ll],
     "sdr_stereo_pcm_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _i, _i, C.c_float, _vp, _vp, _vp, _ll],
+    "sdr_stereo_work_create": [_vp, _i, _ll, _i, _i, _i, C.POINTER(_vp)],
+    "sdr_stereo_work_destroy": [_vp, _vp],
+    "sdr_stereo_front_u8_dev": [_vp, _vp, _ll, _vp, _vp, _vp],
+    "sdr_stereo_back_dev": [_vp, C.c_float, _vp, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
 }
@@ -233,6 +238,18 @@ class ResamplePlan:
         if self._p:
             lib().sdr_resample_plan_destroy(self._ctx._c, self._p)
             self._p = _vp()
+
+
+class StereoWork:
+    """sdr_stereo_work: intermediates of one block for stereo_front/back."""
+
+    def __init__(self, ctx: "Context", w):
+        self._ctx, self._w = ctx, w
+
+    def close(self):
+        if self._w and self._ctx._c:
+            lib().sdr_stereo_work_destroy(self._ctx._c, self._w)
+        self._w = _vp()
 
 
 class Context:
@@ -442,6 +459,23 @@ class Context:
         self._check(lib().sdr_stereo_pcm_u8_dev(self._c, D, _ptr(iq), npairs, nstreams, iq_stride, up, down,
                                                 audio_fs, C.addressof(taps), C.addressof(state), _ptr(pcm),
                                                 pcm_stride), "stereo_pcm_u8_dev")
+
+    def stereo_work(self, D, npairs, up, down, nstreams) -> "StereoWork":
+        """sdr_stereo_work: one block's intermediates for the two-stage stereo calls."""
+        w = _vp()
+        self._check(lib().sdr_stereo_work_create(self._c, D, npairs, up, down, nstreams, C.byref(w)),
+                    "stereo_work_create")
+        return StereoWork(self, w)
+
+    def stereo_front_u8_dev(self, iq, iq_stride, taps, state, work):
+        """Front stage of the stereo path (src/project.cpp:72-121) into `work`."""
+        self._check(lib().sdr_stereo_front_u8_dev(self._c, _ptr(iq), iq_stride, C.addressof(taps),
+                                                  C.addressof(state), work._w), "stereo_front_u8_dev")
+
+    def stereo_back_dev(self, audio_fs, taps, state, work, pcm, pcm_stride):
+        """Back stage (PLL recurrence onwards, :123-132 + 304-314) from `work` to s16 L/R."""
+        self._check(lib().sdr_stereo_back_dev(self._c, audio_fs, C.addressof(taps), C.addressof(state), work._w,
+                                              _ptr(pcm), pcm_stride), "stereo_back_dev")
 
     def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
         self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")

@@ -108,6 +108,9 @@ int sdr_event_create(sdr_ctx *ctx, sdr_event **ev);
 int sdr_event_record(sdr_ctx *ctx, sdr_event *ev);      /* marks the work enqueued so far */
 int sdr_event_synchronize(sdr_ctx *ctx, sdr_event *ev); /* blocks until that work is done */
 int sdr_event_destroy(sdr_ctx *ctx, sdr_event *ev);
+/* The context's stream waits (on the device) for the work an event marked,
+ * which may have been recorded on another context's stream of the same device. */
+int sdr_ctx_wait_event(sdr_ctx *ctx, sdr_event *ev);
 
 /* HIP-graph capture of the context's stream: sdr_graph_begin, then any
  * stream-ordered *_dev / *_async calls (recorded, not run), then
@@ -296,6 +299,26 @@ typedef struct sdr_stereo_state {
 int sdr_stereo_pcm_u8_dev(sdr_ctx *ctx, int D, const uint8_t *iq, long long npairs, int nstreams, long long iq_stride,
                           int up, int down, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
                           int16_t *pcm, long long pcm_stride);
+
+/* The same stereo path in two stages, cut where the PLL recurrence starts,
+ * with one block's intermediates in a work object: sdr_stereo_front_u8_dev
+ * runs the front end, delay + mono resampler and both band-pass filters
+ * (src/project.cpp:72-121); sdr_stereo_back_dev the PLL recurrence, NCO x
+ * stereo band, stereo resampler and the L/R s16 stage (:123-132, 304-314).
+ * The stages touch disjoint parts of the state (front: state_i/q, prev_*,
+ * delay, state_audio, pilot/stereo band-pass; back: pll, stereo_lp_state), so
+ * block b+1's front stage may run on one context's stream while block b's
+ * back stage runs on another's -- order them with sdr_event_record /
+ * sdr_ctx_wait_event and give each block in flight its own work object
+ * (host/sdr_project.cpp).  Outputs equal sdr_stereo_pcm_u8_dev's. */
+typedef struct sdr_stereo_work sdr_stereo_work;
+int sdr_stereo_work_create(sdr_ctx *ctx, int D, long long npairs, int up, int down, int nstreams,
+                           sdr_stereo_work **work);
+int sdr_stereo_work_destroy(sdr_ctx *ctx, sdr_stereo_work *work);
+int sdr_stereo_front_u8_dev(sdr_ctx *ctx, const uint8_t *iq, long long iq_stride, const sdr_stereo_taps *taps,
+                            sdr_stereo_state *state, sdr_stereo_work *work);
+int sdr_stereo_back_dev(sdr_ctx *ctx, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
+                        sdr_stereo_work *work, int16_t *pcm, long long pcm_stride);
 
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the

@@ -121,28 +121,34 @@ def test_reference_project_on_dropin(gpu_ctx, mode, channel):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
-@pytest.mark.parametrize("channel", ["mono", "stereo"])
+@pytest.mark.parametrize("channel", ["mono", "stereo", "stereo-onecall"])
 def test_sdr_project_program(built_lib, oracle, mode, channel):
     """host/sdr_project: src/project.cpp's program with the device block
     pipeline (pinned ring, one stream-ordered call per block).  Same stdout
     bytes as the oracle chain (pinned to the reference program by the CPU
     tests below) -- and as the reference binary itself where it is built --
-    on 2.5 blocks of input: the trailing partial block is dropped and the
-    exit status is 1, as src/project.cpp:293-297 does."""
+    on 5.5 blocks of input: the trailing partial block is dropped and the
+    exit status is 1, as src/project.cpp:293-297 does.  Stereo runs each block
+    as two stages on two contexts' streams, block b+1's front overlapping
+    block b's PLL recurrence (and the ring slots reused: 5 blocks, 2 slots);
+    stereo-onecall is the one-call form (SDR_PROJECT_SPLIT=0)."""
     prog = os.path.join(REPO, "3dy4-real-time-software-defined-radio-_amd", "sdr_project")
     assert os.path.exists(prog), "sdr_project not built"
     from sdrhip.synth import fm_iq_u8
 
+    env = dict(os.environ, SDR_PROJECT_SPLIT="0" if channel == "stereo-onecall" else "1")
+    channel = channel.split("-")[0]
     block_bytes = MODES[mode][5]
     fs = MODES[mode][0]
-    data = fm_iq_u8(block_bytes * 5 // 4, seed=240 + mode, fs=fs).tobytes()
-    r = subprocess.run([prog, str(mode), channel], input=data, capture_output=True)
+    nblk = 5
+    data = fm_iq_u8(block_bytes * (2 * nblk + 1) // 4, seed=240 + mode, fs=fs).tobytes()
+    r = subprocess.run([prog, str(mode), channel], input=data, capture_output=True, env=env)
     assert r.returncode == 1, r.stderr.decode()[-500:]
     assert b"End of input stream reached" in r.stderr
     if channel == "mono":
-        want = _oracle_mono_stream(oracle, mode, data, 2)
+        want = _oracle_mono_stream(oracle, mode, data, nblk)
     else:
-        want, _ = _oracle_stereo_stream(oracle, mode, data, 2)
+        want, _ = _oracle_stereo_stream(oracle, mode, data, nblk)
     assert np.array_equal(np.frombuffer(r.stdout, np.int16), want)
     ref = os.path.join(REPO, "oracle", "_ref", "project_ref")
     if os.path.exists(ref):
@@ -278,12 +284,15 @@ def test_oracle_stereo_chain_equals_reference_program(oracle, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("api", ["one", "split"])
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
-def test_device_stereo_pipeline(gpu_ctx, oracle, built_lib, mode):
-    """sdr_stereo_pcm_u8_dev: independent streams x 3 blocks, u8 IQ in,
-    interleaved s16 L/R out, every byte equal to the oracle chain (pinned to
-    the reference program above), and every carried state -- including the
-    PLL's six floats -- bit-equal after each block."""
+def test_device_stereo_pipeline(gpu_ctx, oracle, built_lib, mode, api):
+    """sdr_stereo_pcm_u8_dev (api one), or sdr_stereo_front_u8_dev +
+    sdr_stereo_back_dev through a work object (api split): independent
+    streams x 3 blocks, u8 IQ in, interleaved s16 L/R out, every byte equal to
+    the oracle chain (pinned to the reference program above), and every
+    carried state -- including the PLL's six floats -- bit-equal after each
+    block."""
     sdrhip = built_lib
     from sdrhip.synth import fm_iq_u8
 
@@ -309,9 +318,16 @@ def test_device_stereo_pipeline(gpu_ctx, oracle, built_lib, mode):
         blk = np.stack([np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
                         for s in range(nstreams)])
         d_iq = A.from_numpy(gpu_ctx, blk)
-        gpu_ctx.stereo_pcm_u8_dev(D, d_iq, npairs, nstreams, 2 * npairs, up, down, audio_fs, t, state, d_pcm,
-                                  pcm_stride)
+        if api == "one":
+            gpu_ctx.stereo_pcm_u8_dev(D, d_iq, npairs, nstreams, 2 * npairs, up, down, audio_fs, t, state, d_pcm,
+                                      pcm_stride)
+        else:
+            work = gpu_ctx.stereo_work(D, npairs, up, down, nstreams)
+            gpu_ctx.stereo_front_u8_dev(d_iq, 2 * npairs, t, state, work)
+            gpu_ctx.stereo_back_dev(audio_fs, t, state, work, d_pcm, pcm_stride)
         gpu_ctx.synchronize()
+        if api == "split":
+            work.close()
         got = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :2 * na]
         for s in range(nstreams):
             want = oracle.stereo(D, blk[s], taps["rf"], ost[s], up, down, taps["audio"], taps["pilot"],
