@@ -15,3 +15,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fu
   -rf --timeout 300 --timeout-method thread -k "f16" > "$OUT/pytest_f16.log" 2>&1
 rc=$?; tail -3 "$OUT/pytest_f16.log"; [ $rc -eq 0 ] || { echo "pytest f16 rc=$rc"; exit $rc; }
 ARMS="SDR_F16_MFMA=1 SDR_F16_MFMA=0" CFGS="cfg5h" REPS=2 bash scripts/sweep_env.sh || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_dropin.py -m gpu -x -q -p no:cacheprovider \
+  -rf --timeout 300 --timeout-method thread -k "stereo or sdr_project" > "$OUT/pytest_stereo.log" 2>&1
+rc=$?; tail -3 "$OUT/pytest_stereo.log"; [ $rc -eq 0 ] || { echo "pytest stereo rc=$rc"; exit $rc; }
+NBLK=3000 REPS=2 timeout -k 10 600 bash scripts/time_project.sh || exit 1

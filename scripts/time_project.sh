@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/time_project
 mkdir -p "$OUT"
 NBLK=${NBLK:-300}
-for mode in 0 2; do
+for mode in ${MODES:-0 2}; do
   python3 - "$mode" "$NBLK" "$OUT/in_$mode.u8" <<'PY'
 import sys
 sys.path.insert(0, "3dy4-real-time-software-defined-radio-_amd")
@@ -19,11 +19,14 @@ fs = {0: 2.4e6, 1: 1.44e6, 2: 2.4e6, 3: 1.92e6}[mode]
 fm_iq_u8(bb * nblk // 2, seed=5, fs=fs).tofile(path)
 PY
   for ch in mono stereo; do
-    for v in ref graph direct; do
+    for v in ref graph direct onecall; do
+      [ $v = onecall ] && [ $ch = mono ] && continue
       case $v in
         ref) prog=oracle/_ref/project_ref; env=;;
         graph) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_NO_GRAPH=0;;
         direct) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_NO_GRAPH=1;;
+        # stereo as one call per block (no overlap of block b+1's front with block b's PLL)
+        onecall) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_SPLIT=0;;
       esac
       # best of REPS runs (each run is a fresh process: HIP init included)
       best=
