@@ -712,6 +712,12 @@ __global__ __launch_bounds__(kPkSlots + 64, 1) void resample_pk2(LpArgs a, PkArg
   const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
   if (i0 >= i1) return;
   auto buf = [&](int it) { return bufs + (it % kPkBufs) * kPkBuf; };
+  // A frame's padded slots may read a few floats past an item's staged span:
+  // they must be finite (zero taps x Inf would poison the sum), so the buffers
+  // start zeroed (and later hold only staged inputs).
+  for (int i = threadIdx.x; i < kPkBufs * kPkBuf / 4; i += kPkSlots + 64)
+    reinterpret_cast<float4*>(bufs)[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  __syncthreads();
   if (loader) lp_stage<CMAX>(a, buf(i0), i0, ln, 64, 0, 1, ln);
   int4 m = make_int4(0, 0, 0, 0);
   f2 tp[U];
