@@ -343,6 +343,8 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // eight copies of the reversed f16 taps, copy q shifted by q halves.
 // Same operands as the dot2 kernel (fp16 x, state and taps), fp32
 // accumulation inside the MFMA: the same tolerance contract.
+// default on once measured on the GPU (SDR_F16_MFMA=1 forces it)
+constexpr int kF16MfmaDefault = 0;
 constexpr int kMfNT = 2;                      // 1,024-output tiles per wave
 constexpr int kMfWaves = 4;                   // one wave per SIMD
 constexpr int kMfOut = 1024 * kMfNT * kMfWaves;  // outputs per workgroup
@@ -491,7 +493,7 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
   // the MFMA form: T % 8 == 0 keeps the staged image's 16-B chunks aligned
   // (x rows are 16-B aligned, checked by the caller); SDR_F16_MFMA=0 selects
   // the dot2 kernel below (A/B, tests)
-  if (ntaps % 8 == 0 && env_int("SDR_F16_MFMA", 1) != 0) {
+  if (ntaps % 8 == 0 && env_int("SDR_F16_MFMA", kF16MfmaDefault) != 0) {
     MfArgs a;
     a.x = static_cast<const _Float16*>(x);
     a.n = n;

@@ -207,7 +207,7 @@ int main(int argc, char* argv[]) {
   // back(b-2) (the slot's previous user), back(b) for front(b).  SDR_PROJECT_SPLIT=0
   // runs the whole block as one call instead.
   const char* spl = std::getenv("SDR_PROJECT_SPLIT");
-  const bool split = !mono && !(spl && std::atoi(spl) == 0);
+  const bool split = !mono && spl && std::atoi(spl) != 0;  // opt-in until measured (SDR_PROJECT_SPLIT=1)
   sdr_ctx* g_back = nullptr;
   sdr_stereo_work* work[2] = {nullptr, nullptr};
   sdr_event* front_done[2] = {nullptr, nullptr};
