@@ -23,8 +23,8 @@ PY
       [ $v = onecall ] && [ $ch = mono ] && continue
       case $v in
         ref) prog=oracle/_ref/project_ref; env=;;
-        graph) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_NO_GRAPH=0;;
-        direct) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_NO_GRAPH=1;;
+        graph) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=0 SDR_PROJECT_SPLIT=1";;
+        direct) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=1 SDR_PROJECT_SPLIT=1";;
         # stereo as one call per block (no overlap of block b+1's front with block b's PLL)
         onecall) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_SPLIT=0;;
       esac
