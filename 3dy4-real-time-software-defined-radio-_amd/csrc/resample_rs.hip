@@ -616,231 +616,6 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   }
 }
 
-// ---------------------------------------------------------- resample_pk2 --
-// Two phases per lane, packed.  resample_lp reads 4 B of LDS per
-// multiply-add (one ds_read_b128 per 4 taps of one column) and issues two
-// VALU instructions per multiply-add from each wave, and both counts bound
-// it.  Adjacent phases phi, phi+1 read windows d =
-// q(phi+1) - q(phi) = floor/ceil(M/L) inputs apart (5-6 at 147/800), so one
-// staged input feeds both: one v_pk_mul_f32 (tap pair x the input in both
-// halves) and one v_pk_add_f32 (the two running sums) per input -- half the
-// LDS bytes and half the issue slots per multiply-add, the same SIMD cycles.
-// Two full tap rows do not fit the VGPRs, so each row is split at C0 =
-// (CMAX+1)/2: lane 2j holds both phases' taps c < C0, lane 2j+1 the rest,
-// each as a frame of U slots aligned to 16-B chunks of the staged inputs
-// (zero taps outside a phase's part of the frame).  A column's sums run in
-// the reference's order: the even lane takes c = 0..C0-1 at step s, hands
-// both partial sums to the odd lane (DPP), which continues c = C0..CMAX-1 at
-// step s+1 and stores.  Items (C columns of one stream) rotate through three
-// LDS buffers: at step s the even lanes read item s, the odd lanes item s-1,
-// the loader wave stages item s+1.
-// Zero taps times finite inputs add +-0, which changes no bit of a sum that
-// starts at +0.0f; an infinite or NaN input in a padded slot would, so an
-// output that comes out non-finite is recomputed from the staged span by the
-// plain sequential loop (the reference's own order and terms).
-// f(integral_constant<int, B>), ..., f(<E-1>): an unrolled loop with a constant index
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-constexpr int kPkWaves = 7;
-constexpr int kPkSlots = 64 * kPkWaves;
-constexpr int kPkBufs = 3;
-constexpr int kPkBuf = 12800;  // floats per buffer (50 KiB, a multiple of 256 B: bank-aligned)
-constexpr int kPkK = 4;        // columns (chains) per lane per item
-
-template <int CMAX>
-struct PkGeom {
-  static constexpr int C0 = (CMAX + 1) / 2;
-  static constexpr int DMAX = CMAX == 151 ? 9 : 10;  // largest d the frame holds
-  static constexpr int U = (C0 + 3 + DMAX + 3) / 4 * 4;  // frame slots (88 at 151, 64 at 101)
-};
-
-struct PkArgs {
-  const float* tab;  // [kPkSlots][U] tap pairs (phase a, phase b), interleaved
-  const int4* meta;  // [kPkSlots]: phi_a, valid, half | sub << 8, frame chunk offset
-  const float* h;    // the taps (non-finite recompute)
-};
-
-template <int CMAX>
-__global__ __launch_bounds__(256) void build_pk2_tables(const float* __restrict__ h, int up, int down, int S,
-                                                        float* __restrict__ tab, int4* __restrict__ meta) {
-  using G = PkGeom<CMAX>;
-  constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= kPkSlots * G::U) return;
-  const int t = idx / G::U, u = idx - t * G::U;
-  const int P = (up + 1) / 2;  // phase pairs
-  const int j = t >> 1, half = t & 1;
-  const int pi = j % P, sub = j / P;
-  const bool valid = sub < S;
-  const int pa = 2 * pi;
-  const bool has_b = pa + 1 < up;
-  const int qa = (int)((long long)pa * down / up);
-  const int d = has_b ? (int)((long long)(pa + 1) * down / up) - qa : 0;
-  const int clo = half ? G::C0 : 0, chi = half ? CMAX : G::C0;
-  const int A = ((qa - chi + 1 - base0) % 4 + 4) % 4;
-  const int f0 = qa - chi + 1 - A;  // input index of frame slot 0 (relative to the column start)
-  // slot u <-> input f0 + u: phase a tap c = qa - f0 - u, phase b tap c = qa + d - f0 - u
-  const int ca = qa - f0 - u, cb = qa + d - f0 - u;
-  const int pha = (int)((long long)pa * down % up), phb = (int)((long long)(pa + 1) * down % up);
-  float ta = 0.0f, tb = 0.0f;
-  if (valid && ca >= clo && ca < chi) ta = h[pha + (long long)ca * up];
-  if (valid && has_b && cb >= clo && cb < chi) tb = h[phb + (long long)cb * up];
-  tab[2 * idx] = ta;
-  tab[2 * idx + 1] = tb;
-  if (u == 0) meta[t] = make_int4(pa, valid ? 1 : 0, half | (sub << 8), (f0 - base0) >> 2);
-}
-
-template <int CMAX, int K>
-__global__ __launch_bounds__(kPkSlots + 64, 1) void resample_pk2(LpArgs a, PkArgs pk) {
-  using G = PkGeom<CMAX>;
-  constexpr int U = G::U, NCH = U / 4;
-  constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
-  __shared__ __attribute__((aligned(16))) float bufs[kPkBufs * kPkBuf];
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) const f4v lds4;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-  const bool loader = wv == kPkWaves;
-  const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
-  const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
-  const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
-  if (i0 >= i1) return;
-  auto buf = [&](int it) { return bufs + (it % kPkBufs) * kPkBuf; };
-  // A frame's padded slots may read a few floats past an item's staged span:
-  // they must be finite (zero taps x Inf would poison the sum), so the buffers
-  // start zeroed (and later hold only staged inputs).
-  for (int i = threadIdx.x; i < kPkBufs * kPkBuf / 4; i += kPkSlots + 64)
-    reinterpret_cast<float4*>(bufs)[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  __syncthreads();
-  if (loader) lp_stage<CMAX>(a, buf(i0), i0, ln, 64, 0, 1, ln);
-  int4 m = make_int4(0, 0, 0, 0);
-  f2 tp[U];
-  if (!loader) {
-    m = pk.meta[threadIdx.x];
-    const float4* row = reinterpret_cast<const float4*>(pk.tab + (long long)threadIdx.x * 2 * U);
-#pragma unroll
-    for (int u = 0; u < U; u += 2) {
-      const float4 v = row[u / 2];
-      tp[u] = f2{v.x, v.y};
-      tp[u + 1] = f2{v.z, v.w};
-    }
-  }
-  const int pa = m.x, half = m.z & 0xff, sub = m.z >> 8, f0c = m.w;
-  const bool valid = m.y != 0;
-  f2 acc[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) acc[k] = f2{0.0f, 0.0f};
-  for (int s = i0; s <= i1; ++s) {
-    if (loader) dma_drain();
-    __syncthreads();  // item s is staged; buffer (s+1) % 3's last reader (odd lanes, item s-2) is done
-    if (loader) {
-      if (s < i1 && s % a.nbat == 0) {  // the stream's first item: its span holds the old state; commit
-        const long long st = s / a.nbat;
-        for (int j = ln; j < a.ns; j += 64) a.state[st * a.ns + j] = a.x[st * a.x_stride + (a.n - a.ns) + j];
-      }
-      if (s + 1 < i1) lp_stage<CMAX>(a, buf(s + 1), s + 1, ln, 64, 0, 1, ln);
-      continue;
-    }
-    const int it = half ? s - 1 : s;  // the item this lane works on
-    const bool live = it >= i0 && it < i1;
-    const int stv = live ? it / a.nbat : 0, b = live ? it - stv * a.nbat : 0;
-    const int t0 = b * a.C;
-    const int ce = live ? min(a.C, a.np - t0) : 0;
-    if (!half) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] = f2{0.0f, 0.0f};
-    }
-    if (live) {
-      const float* bp = buf(it);
-      lds4* ptr[K];
-      bool act[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int c = sub + a.S * k;
-        act[k] = valid && c < ce;
-        const int cc = c < ce ? c : ((c & 1) < ce ? (c & 1) : 0);
-        ptr[k] = (lds4*)(bp + 4 * (cc * (a.down >> 2) + f0c));
-        asm volatile("" : "+v"(ptr[k]));
-      }
-      f4v cur[K], nxt[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) cur[k] = ptr[k][NCH - 1];
-#pragma unroll
-      for (int ch = NCH - 1; ch >= 0; --ch) {
-        if (ch > 0) {
-#pragma unroll
-          for (int k = 0; k < K; ++k) nxt[k] = ptr[k][ch - 1];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // element jj of a staged chunk is half (jj & 1) of the aligned register
-        // pair (jj & 2, jj | 1): op_sel picks it for both product lanes
-        static_for<0, 4>([&](auto jx) {
-          constexpr int jj = 3 - decltype(jx)::value;
-          const int u = 4 * ch + jj;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const f2 xp = (jj & 2) ? f2{cur[k].z, cur[k].w} : f2{cur[k].x, cur[k].y};
-            f2 prod;
-            if constexpr (jj & 1)
-              asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(prod) : "v"(xp), "v"(tp[u]));
-            else
-              asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(prod) : "v"(xp), "v"(tp[u]));
-            acc[k] = acc[k] + prod;
-          }
-        });
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          cur[k] = nxt[k];
-          asm volatile("" : "+v"(acc[k]));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (half) {
-        // the column's outputs phi_a, phi_a + 1 (src/filter.cpp:160-166 order, both halves)
-        float* ys = a.y + (long long)stv * a.y_stride;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          if (!act[k]) continue;
-          const int cc = sub + a.S * k;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int phi = pa + e;
-            const long long j = (long long)a.up * (t0 + cc) + phi;
-            if (phi >= a.up || j >= a.ny) continue;
-            float y = e ? acc[k].y : acc[k].x;
-            if (!__builtin_isfinite(y)) {
-              // a padded slot may have met an Inf / NaN: the plain sequential sum
-              const int q = (int)((long long)phi * a.down / a.up), p = (int)((long long)phi * a.down % a.up);
-              const float* col = bp + cc * a.down - base0 + q;
-              y = 0.0f;
-              for (int c = 0; c < CMAX; ++c) y = y + pk.h[p + (long long)c * a.up] * col[-c];
-            }
-            ys[j] = y;
-          }
-        }
-      }
-    }
-    // hand-off: odd lanes take their even partner's partial sums for the next step
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int rx = __builtin_amdgcn_update_dpp(0, __float_as_int(acc[k].x), 0xA0, 0xf, 0xf, false);
-      const int ry = __builtin_amdgcn_update_dpp(0, __float_as_int(acc[k].y), 0xA0, 0xf, 0xf, false);
-      if (half) acc[k] = f2{__int_as_float(rx), __int_as_float(ry)};
-    }
-  }
-}
-
-bool pk2_enabled() {
-  const char* e = std::getenv("SDR_RESAMPLE_PK2");
-  return e && std::atoi(e) != 0;
-}
-
 // read per launch (a getenv scan), so a test can switch kernels in-process
 bool lp_enabled() {
   const char* e = std::getenv("SDR_RESAMPLE_LP");
@@ -861,51 +636,10 @@ bool rs_enabled() {
 
 }  // namespace
 
-// resample_pk2's tables sit behind resample_lp's (shifted rows + lane table)
-size_t pk2_tables_offset(int up, int ntaps) {
-  const int cmax = (ntaps + up - 1) / up;
-  const int U = (cmax + 3 + 3) / 4 * 4;
-  return ((size_t)4 * up * U + kLpSlots + 3) / 4 * 4;
-}
-
 size_t resample_rs_scratch_floats(int up, int ntaps) {
   const int cmax = (ntaps + up - 1) / up;
-  const int Upk = cmax == 151 ? PkGeom<151>::U : PkGeom<101>::U;
-  return pk2_tables_offset(up, ntaps) + (size_t)kPkSlots * 2 * Upk + (size_t)kPkSlots * 4;
-}
-
-// resample_pk2's shape: the frame must hold d <= ceil(M/L), the staging buffer an
-// item's span, and (as resample_lp) a stream's second item must not
-// start inside the carried state.  Returns the columns per item, 0 = not covered.
-int pk2_columns(int up, int down, int cmax, int ns, long long ny) {
-  if (!(cmax == 151 || cmax == 101) || up < 2 || up > kPkSlots || down % 4 || (long long)up * down >= (1LL << 31))
-    return 0;
-  const int dmax = cmax == 151 ? PkGeom<151>::DMAX : PkGeom<101>::DMAX;
-  if ((down + up - 1) / up > dmax || ns > 4096) return 0;
-  const int base0 = -(((cmax - 1) + 3) / 4 * 4);
-  const int qmax = (int)((long long)(up - 1) * down / up);
-  if (qmax + 1 - base0 + 4 > kPkBuf) return 0;
-  const int S = kPkSlots / (2 * ((up + 1) / 2));
-  const int np = (int)((ny + up - 1) / up);
-  int C = S * kPkK;
-  const long long fit = (kPkBuf - (qmax + 1 - base0) - 4) / down + 1;
-  if (C > fit) C = (int)fit;
-  if (C > np) C = np;
-  if (C < 1) return 0;
-  if (np > C && (long long)C * down + base0 < 0) return 0;
-  return C;
-}
-
-void build_pk2(int cmax, const float* h, int up, int down, float* tables, hipStream_t st) {
-  const int S = kPkSlots / (2 * ((up + 1) / 2));
-  const int U = cmax == 151 ? PkGeom<151>::U : PkGeom<101>::U;
-  float* tab = tables;
-  int4* meta = reinterpret_cast<int4*>(tables + (size_t)kPkSlots * 2 * U);
-  const dim3 g((unsigned)((kPkSlots * U + 255) / 256));
-  if (cmax == 151)
-    hipLaunchKernelGGL(build_pk2_tables<151>, g, dim3(256), 0, st, h, up, down, S, tab, meta);
-  else
-    hipLaunchKernelGGL(build_pk2_tables<101>, g, dim3(256), 0, st, h, up, down, S, tab, meta);
+  const int U = (cmax + 3 + 3) / 4 * 4;
+  return (size_t)4 * up * U + kLpSlots;  // shifted rows (+ resample_lp's lane table)
 }
 
 // Returns false (nothing launched) when the shape is not one this kernel
@@ -924,10 +658,6 @@ bool resample_lp_tables(int up, int down, const float* h, int ntaps, int ns, flo
   int* lanes = reinterpret_cast<int*>(tables + tab);
   hipLaunchKernelGGL(build_lp_tables, dim3((unsigned)((tab + kLpSlots - 1) / kLpSlots + 1)), dim3(kLpSlots), 0, st, h,
                      up, down, cmax, U, S, base0, tables, lanes);
-  // and resample_pk2's, where it covers the shape (ns and ny are not known
-  // here: pk2_columns is checked again per call)
-  if (pk2_columns(up, down, cmax, 0, (long long)up * 2) > 0)
-    build_pk2(cmax, h, up, down, tables + pk2_tables_offset(up, ntaps), st);
   *err = hipGetLastError();
   return true;
 }
@@ -961,49 +691,7 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   // reader of the old state, i.e. the second item's span starts at p >= 0
   // (up = 128, down = 4 gives C = 21, P0 = 21*4 - 152 < 0).
   if (use_lp && np > lpC && (long long)lpC * down + base0 < 0) use_lp = false;
-  static const int ablate0 = env_int("SDR_ABLATE", 0);
-  // resample_pk2 (SDR_RESAMPLE_PK2=1): phase pairs, packed (see the kernel)
-  const int pkC = pk2_enabled() ? pk2_columns(up, down, cmax, ns, ny) : 0;
-  if (pkC > 0) {
-    LpArgs b;
-    b.x = x;
-    b.n = n;
-    b.x_stride = x_stride;
-    b.hs = nullptr;
-    b.lanes = nullptr;
-    b.up = up;
-    b.down = down;
-    b.state = state;
-    b.ns = ns;
-    b.y = y;
-    b.y_stride = y_stride;
-    b.ny = ny;
-    b.np = np;
-    b.C = pkC;
-    b.nbat = (np + pkC - 1) / pkC;
-    b.nitems = b.nbat * nstreams;
-    b.S = kPkSlots / (2 * ((up + 1) / 2));
-    b.ablate = ablate0;
-    const float* tables = (lp_tables ? lp_tables : scratch) + pk2_tables_offset(up, ntaps);
-    if (!lp_tables) {
-      build_pk2(cmax, h, up, down, const_cast<float*>(tables), st);
-      if ((*err = hipGetLastError()) != hipSuccess) return true;
-    }
-    const int U = cmax == 151 ? PkGeom<151>::U : PkGeom<101>::U;
-    PkArgs pk;
-    pk.tab = tables;
-    pk.meta = reinterpret_cast<const int4*>(tables + (size_t)kPkSlots * 2 * U);
-    pk.h = h;
-    const int ncu0 = device_cu_count();
-    const dim3 g((unsigned)(b.nitems < ncu0 ? b.nitems : ncu0));
-    if (cmax == 151)
-      hipLaunchKernelGGL((resample_pk2<151, kPkK>), g, dim3(kPkSlots + 64), 0, st, b, pk);
-    else
-      hipLaunchKernelGGL((resample_pk2<101, kPkK>), g, dim3(kPkSlots + 64), 0, st, b, pk);
-    *err = hipGetLastError();
-    *state_done = true;  // the loader commits the state
-    return true;
-  }
+
   // resample_rs: the ring must hold a group's whole window plus the next group's new inputs
   const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
   const long long step = ((long long)kRsPG * down + up - 1) / up + 8;

@@ -220,16 +220,13 @@ def test_cfg5_full_windows(gpu_ctx, oracle, built_lib):
     assert_bits(d_st.download().reshape(2, T - 1), x[:, n - (T - 1):], "state")
 
 
-@pytest.mark.parametrize("kernel", ["default", "pk2"])
-def test_cfg3_full_plan_two_steps(gpu_ctx, oracle, built_lib, monkeypatch, kernel):
+def test_cfg3_full_plan_two_steps(gpu_ctx, oracle, built_lib):
     """BASELINE config 3 exactly as bench.py launches it: 1,024 streams x
     65,600 samples through a resampler plan built from the real
     impulseResponseLPF(240e3*147, 16e3, 22197, 147) taps (151 per phase, S =
     150), two consecutive steps with the state carried.  EVERY stream's
     12,054 outputs and carried state bitwise against the oracle
-    (src/filter.cpp:142-173) -- the workgroup item split at 1,024 streams.
-    kernel pk2: resample_pk2 (SDR_RESAMPLE_PK2=1)."""
-    monkeypatch.setenv("SDR_RESAMPLE_PK2", "1" if kernel == "pk2" else "0")
+    (src/filter.cpp:142-173) -- the workgroup item split at 1,024 streams."""
     sdrhip = built_lib
     S, n, up, down, T, ns = 1024, 65600, 147, 800, 151 * 147, 150
     ny = sdrhip.resample_out_len(up, down, n)

@@ -170,8 +170,7 @@ RESAMPLE_CASES = [(147, 800, 151, 150, 1600), (147, 1280, 101, 100, 2560), (3, 7
                   (128, 4, 151, 150, 640)]
 # resample_lp with its loader wave (the default) and without, then resample_rs,
 # then the phase-major resample_pp
-RESAMPLE_KERNELS = {"pk2": {"SDR_RESAMPLE_PK2": "1"},
-                    "lpw": {"SDR_RESAMPLE_LOADER": "1"}, "lp": {"SDR_RESAMPLE_LOADER": "0"},
+RESAMPLE_KERNELS = {"lpw": {"SDR_RESAMPLE_LOADER": "1"}, "lp": {"SDR_RESAMPLE_LOADER": "0"},
                     "rs": {"SDR_RESAMPLE_LP": "0"},
                     "pp": {"SDR_RESAMPLE_LP": "0", "SDR_RESAMPLE_RS": "0"}}
 
@@ -209,7 +208,7 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
         assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
 
 
-@pytest.mark.parametrize("kernel", ["pk2", "lpw", "lp", "rs"])
+@pytest.mark.parametrize("kernel", ["lpw", "lp", "rs"])
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 8000), (147, 1280, 101, 100, 12800)])
 def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
     """Inf and NaN inputs (and in the carried state): every output equals the
@@ -246,14 +245,12 @@ def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, monkeypatch, kern
 
 @pytest.mark.parametrize("up,down,cnt,nstreams,n", [(147, 800, 151, 130, 8000), (147, 800, 101, 64, 4000),
                                                      (441, 3200, 101, 70, 6400), (147, 1280, 101, 3, 25600)])
-@pytest.mark.parametrize("kernel", ["default", "pk2"])
-def test_resample_many_streams(gpu_ctx, oracle, built_lib, monkeypatch, up, down, cnt, nstreams, n, kernel):
-    """The default resampler (and resample_pk2) over many streams per launch
-    (64-130: several workgroups' item ranges, items starting inside the
-    carried state, a ragged last batch) and over few long streams; three
-    consecutive blocks, state carried; checked stream by stream against the
-    oracle (a random sample of streams when there are many)."""
-    monkeypatch.setenv("SDR_RESAMPLE_PK2", "1" if kernel == "pk2" else "0")
+def test_resample_many_streams(gpu_ctx, oracle, built_lib, up, down, cnt, nstreams, n):
+    """The default resampler over many streams per launch (64-130: several
+    workgroups' item ranges, items starting inside the carried state, a
+    ragged last batch) and over few long streams; three consecutive blocks,
+    state carried; checked stream by stream against the oracle (a random
+    sample of streams when there are many)."""
     sdrhip = built_lib
     rng = np.random.default_rng(up + down + nstreams)
     h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
@@ -661,13 +658,11 @@ def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch
 
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 65600), (147, 800, 101, 100, 8000),
                                              (147, 1280, 101, 100, 12800), (3, 5, 101, 100, 5000)])
-@pytest.mark.parametrize("kernel", ["default", "pk2"])
-def test_resample_plan_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, up, down, cnt, ns, n, kernel):
+def test_resample_plan_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, n):
     """sdr_resample_plan_*: the lane-phase tables built once at plan creation,
     then three consecutive blocks through the plan -- outputs and carried
     state bitwise against the oracle.  (3, 5) is a shape the lane-phase
     kernel does not take: the plan falls back to the per-call path."""
-    monkeypatch.setenv("SDR_RESAMPLE_PK2", "1" if kernel == "pk2" else "0")
     sdrhip = built_lib
     nstreams = 3
     rng = np.random.default_rng(up + down + cnt)
