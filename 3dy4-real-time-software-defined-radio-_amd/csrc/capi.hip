@@ -759,6 +759,8 @@ int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const floa
   return SDR_OK;
 }
 
+int sdr_fir_block_f16_kernel(int ntaps) { return sdr::fir_f16_uses_mfma(ntaps) ? 1 : 0; }
+
 int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,
                           int ntaps, void* state, int ns, float* y, long long y_stride) {
   int rc = enter(c);

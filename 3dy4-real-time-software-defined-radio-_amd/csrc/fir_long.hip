@@ -485,6 +485,8 @@ __global__ __launch_bounds__(kWG) void f32_to_f16(const float* __restrict__ x, l
 
 }  // namespace
 
+bool fir_f16_uses_mfma(int ntaps) { return ntaps % 8 == 0 && env_int("SDR_F16_MFMA", kF16MfmaDefault) != 0; }
+
 size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32); }
 
 hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
@@ -493,7 +495,7 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
   // the MFMA form: T % 8 == 0 keeps the staged image's 16-B chunks aligned
   // (x rows are 16-B aligned, checked by the caller); SDR_F16_MFMA=0 selects
   // the dot2 kernel below (A/B, tests)
-  if (ntaps % 8 == 0 && env_int("SDR_F16_MFMA", kF16MfmaDefault) != 0) {
+  if (fir_f16_uses_mfma(ntaps)) {
     MfArgs a;
     a.x = static_cast<const _Float16*>(x);
     a.n = n;

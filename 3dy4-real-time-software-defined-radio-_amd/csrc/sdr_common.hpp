@@ -127,6 +127,8 @@ hipError_t launch_fir_long(const FirLaunch& a, const float* h, hipStream_t st);
 // [nstreams][x_stride] / [nstreams][ns], y fp32; scratch_pairs holds
 // fir_long_h_pairs(ntaps) packed tap pairs.
 size_t fir_long_h_pairs(int ntaps);
+// whether sdr_fir_block_f16_dev runs the MFMA kernel for ntaps (else v_dot2)
+bool fir_f16_uses_mfma(int ntaps);
 hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
                              void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
                              hipStream_t st);

@@ -95,6 +95,7 @@ _SIGS = {
     "sdr_resample_plan_destroy": [_vp, _vp],
     "sdr_fir_block_f16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
     "sdr_f32_to_f16_dev": [_vp, _vp, _ll, _vp],
+    "sdr_fir_block_f16_kernel": [_i],
     "sdr_delay_f32_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
     "sdr_pcm_s16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _ll],
     "sdr_mono_pcm_u8_dev": [_vp, _i, _vp, _ll, _i, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _i,
@@ -238,6 +239,29 @@ class ResamplePlan:
         if self._p:
             lib().sdr_resample_plan_destroy(self._ctx._c, self._p)
             self._p = _vp()
+
+
+class Event:
+    """sdr_event: marks the work enqueued on a context's stream so far."""
+
+    def __init__(self, ctx: "Context"):
+        self._ctx, self._e = ctx, _vp()
+        ctx._check(lib().sdr_event_create(ctx._c, C.byref(self._e)), "event_create")
+
+    def record(self, ctx: "Context"):
+        ctx._check(lib().sdr_event_record(ctx._c, self._e), "event_record")
+
+    def wait(self, ctx: "Context"):
+        """ctx's stream waits (on the device) for the recorded work (sdr_ctx_wait_event)."""
+        ctx._check(lib().sdr_ctx_wait_event(ctx._c, self._e), "ctx_wait_event")
+
+    def synchronize(self):
+        self._ctx._check(lib().sdr_event_synchronize(self._ctx._c, self._e), "event_synchronize")
+
+    def close(self):
+        if self._e and self._ctx._c:
+            lib().sdr_event_destroy(self._ctx._c, self._e)
+        self._e = _vp()
 
 
 class StereoWork:

@@ -52,6 +52,7 @@ sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 FP32_VALU_PEAK_TFLOPS = 157.3
+F16_MFMA_PEAK_TFLOPS = 2500.0  # dense FP16 MFMA (MI355X_MICROARCH.md chip table; not the 2:1-sparse figure)
 # discriminator per decimated output (src/filter.cpp:88-98): I*I + Q*Q (3), the two
 # differences and products (4), a - b and the divide (2)
 DEMOD_FLOP = 9.0
@@ -107,6 +108,9 @@ def parse(argv=None):
     ap.add_argument("--batches", type=int, default=2, help="distinct input batches the steps cycle over")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per replayed HIP graph")
     ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
+    ap.add_argument("--stereo-pipeline", type=int, default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "0")),
+                    help="stereo configs: 1 = each step as two stages on two contexts' streams (front end + band-pass "
+                         "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
                     help="after the timed window, time this many seconds of back-to-back steps (the "
                          "`sustained` field: a receiver runs the block loop continuously); 0 skips it")
@@ -313,6 +317,35 @@ class Job:
                                          sbuf["stereo"].data_ptr(), 100, sbuf["pll"].data_ptr())
             pcm = torch.empty(S * 2 * na, dtype=torch.int16, device=dev)
             self.keep += [sbuf, taps_s, state_s, pcm, d_ha, d_hp, d_hs]
+            if args.stereo_pipeline:
+                # the step cut where the PLL recurrence starts (sdr_stereo_front_u8_dev |
+                # sdr_stereo_back_dev, disjoint state): front stages on this context's
+                # stream, back stages on a second context's, two work objects in a ring --
+                # front(b) waits for back(b-2), back(b) for front(b) (host/sdr_project.cpp)
+                ctx2 = self.ctx2 = sdrhip.Context(device)
+                self.stream2 = torch.cuda.Stream(dev)
+                ctx2.set_stream(self.stream2.cuda_stream)
+                works = [ctx.stereo_work(D, n, up, down, S) for _ in range(2)]
+                ev_f = [sdrhip.Event(ctx) for _ in range(2)]
+                ev_b = [sdrhip.Event(ctx) for _ in range(2)]
+                self.keep += [works, ev_f, ev_b]
+
+                def seq(j0, k):
+                    """k consecutive steps; the first two wait on nothing (whatever ran
+                    before has completed: a graph replay or a synchronised direct run),
+                    and the sequence ends with this stream joined to the back stages."""
+                    for j in range(k):
+                        slot = (j0 + j) % 2
+                        if j >= 2:
+                            ev_b[slot].wait(ctx)
+                        ctx.stereo_front_u8_dev(iqs[(j0 + j) % len(iqs)], 2 * n, taps_s, state_s, works[slot])
+                        ev_f[slot].record(ctx)
+                        ev_f[slot].wait(ctx2)
+                        ctx2.stereo_back_dev(240e3, taps_s, state_s, works[slot], pcm, 2 * na)
+                        ev_b[slot].record(ctx2)
+                    if k:
+                        ev_b[(j0 + k - 1) % 2].wait(ctx)
+                self.seq = seq
             for iq in iqs:
                 steps.append(lambda iq=iq: ctx.stereo_pcm_u8_dev(D, iq, n, S, 2 * n, up, down, 240e3, taps_s,
                                                                  state_s, pcm, 2 * na))
@@ -402,6 +435,7 @@ class Job:
             torch.cuda.synchronize(dev)
             err = float((got - ref).abs().max())
             scale = float(d_h.abs().sum()) * float(IQ.abs().max())
+            self.f16_kernel = "mfma" if sdrhip.lib().sdr_fir_block_f16_kernel(T) else "dot2"
             self.tolerance = {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale,
                               "norm": "sum|h| * max|x|", "rms_err": float((got - ref).pow(2).mean().sqrt())}
         self.steps = steps
@@ -417,11 +451,16 @@ class Job:
             while k - i >= gs:
                 g.launch()
                 i += gs
-        for j in range(i, k):
-            self.steps[(self._next + j) % len(self.steps)]()
+        if self.seq is not None:
+            self.seq(self._next + i, k - i)
+        else:
+            for j in range(i, k):
+                self.steps[(self._next + j) % len(self.steps)]()
         self._next = (self._next + k) % len(self.steps)
 
     _next = 0
+    seq = None  # a step sequencer (two-stage stereo pipeline) instead of one call per step
+    ctx2 = None
 
     def capture(self, gs: int):
         """Record gs consecutive steps into a HIP graph (gs a multiple of the batch
@@ -431,7 +470,12 @@ class Job:
         nb = len(self.steps)
         gs = max(nb, gs - gs % nb)
         self._next = 0
-        self.graph = (self.ctx.capture(lambda: [self.steps[j % nb]() for j in range(gs)]), gs)
+        if self.seq is not None:
+            self.graph = (self.ctx.capture(lambda: self.seq(0, gs)), gs)
+            # the back stages' context: its scratch must not grow under the graph
+            self.ctx2.pin_scratch(True)
+        else:
+            self.graph = (self.ctx.capture(lambda: [self.steps[j % nb]() for j in range(gs)]), gs)
 
     def warm(self, warmup: int, seconds: float):
         """W warmup steps, then more of the same launches until >= seconds of
@@ -479,8 +523,11 @@ class Job:
             self.graph = None
         self.torch.cuda.synchronize(self.dev)
         for k in self.keep:
-            if hasattr(k, "close"):
-                k.close()
+            for obj in (k if isinstance(k, list) else [k]):
+                if hasattr(obj, "close"):
+                    obj.close()
+        if self.ctx2 is not None:
+            self.ctx2.close()
         self.ctx.close()
 
 
@@ -514,8 +561,8 @@ def run_device(cfg_name, device, seed, args, barrier=None, side=True):
             job.warm(0, args.warm_seconds)
             res["fma_ms"], _ = job.timed(args.steps)
             job.ctx.set_arith(job.sdrhip.ARITH_EXACT)
-        res["job"] = {k: getattr(job, k) for k in ("units", "bytes_per_pair", "flops_per_unit", "metric", "bound",
-                                                  "kind", "tolerance")}
+        res["job"] = {k: getattr(job, k, None) for k in ("units", "bytes_per_pair", "flops_per_unit", "metric",
+                                                        "bound", "kind", "tolerance", "f16_kernel")}
     finally:
         job.close()
     return res
@@ -530,7 +577,10 @@ def roofline(job: dict, ms_per_step: float, config: str, arith: str = "exact") -
     and the fp16 arm's v_dot2_f32_f16 two multiply-adds per issue."""
     launch_s = ms_per_step * 1e-3
     units = job["units"]
-    if job["kind"] == "fir_block_f16":
+    f16_mfma = job["kind"] == "fir_block_f16" and job.get("f16_kernel") == "mfma"
+    if f16_mfma:
+        vpeak = F16_MFMA_PEAK_TFLOPS
+    elif job["kind"] == "fir_block_f16":
         vpeak = FP32_VALU_PEAK_TFLOPS * 2
     elif arith == "fma":
         vpeak = FP32_VALU_PEAK_TFLOPS
@@ -550,7 +600,9 @@ def roofline(job: dict, ms_per_step: float, config: str, arith: str = "exact") -
     roof["hbm_frac"] = round(hbm_frac, 4)
     roof["valu_frac"] = round(valu_frac, 4)
     roof["valu_peak_tflops"] = round(vpeak, 2)
-    roof["arith"] = arith if job["kind"] != "fir_block_f16" else "f16 storage, f32 dot2 accumulation"
+    roof["arith"] = (arith if job["kind"] != "fir_block_f16" else
+                     "f16 storage, f32 accumulation on v_mfma_f32_32x32x16_f16 (dense peak)" if f16_mfma else
+                     "f16 storage, f32 dot2 accumulation")
     traffic = None
     tpath = os.path.join(REPO, "profiles", f"traffic_{config}.json")
     if os.path.exists(tpath):
@@ -659,6 +711,9 @@ def main(argv=None):
                                       f"({'one host thread per device' if plan['mode'] == 'threads' else 'one process per device, gloo timing barrier'})",
                        "devices_opened": distinct, "input_batches": max(1, args.batches),
                        "launch": "direct" if args.no_graph else f"HIP graph of {args.graph_steps} steps",
+                       **({"stereo_pipeline": "two stages on two contexts' streams (front | PLL onwards), step b+1's "
+                                              "front overlapping step b's recurrence" if args.stereo_pipeline
+                           else "one call per step"} if job["kind"] == "stereo_u8" else {}),
                        "state_carried_across_steps": True,
                        "arith": ("fma: one fused multiply-add per tap, tolerance-tested (DESIGN.md 2)"
                                  if args.arith == "fma" else "exact: the reference's bits")},

@@ -223,6 +223,9 @@ int sdr_resample_plan_destroy(sdr_ctx *ctx, sdr_resample_plan *plan);
  * products (v_dot2_f32_f16).  NOT bit-exact with the reference -- a
  * tolerance arm; the fp32 calls above are the exact path.  Rows must be
  * 16-B aligned. */
+/* Which kernel sdr_fir_block_f16_dev runs for ntaps under the current
+ * environment: 1 = the Toeplitz GEMM on v_mfma_f32_32x32x16_f16, 0 = v_dot2. */
+int sdr_fir_block_f16_kernel(int ntaps);
 int sdr_fir_block_f16_dev(sdr_ctx *ctx, const void *x, long long n, int nstreams, long long x_stride,
                           const float *h, int ntaps, void *state, int ns, float *y, long long y_stride);
 /* fp32 -> fp16 (round to nearest even), count elements, stream-ordered. */

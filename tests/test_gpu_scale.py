@@ -338,3 +338,78 @@ def test_long_stream_segments_two_threads(built_lib, oracle, D, T, ns):
     want = oracle.frontend(D, I, Q, h, si, sq, pv)
     assert_bits(got, want, "stitched segments vs the oracle")
     assert_bits(res[1][3], pv, "prev vs the oracle")
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
+    """bench.py --stereo-pipeline's schedule (and sdr_project's): each block as
+    sdr_stereo_front_u8_dev on one context's stream and sdr_stereo_back_dev on
+    a second context's, two work objects in a ring, front(b) waiting for
+    back(b-2) and back(b) for front(b) by sdr_ctx_wait_event -- block b+1's
+    front overlapping block b's PLL recurrence.  128 streams x 5 mode-0
+    blocks, direct or captured as one HIP graph spanning both streams:
+    every PCM byte and every carried state word against the oracle chain."""
+    sdrhip = built_lib
+    mode, nstreams, nblk = 0, 128, 5
+    rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
+    npairs = block_bytes // 2
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb:  # each on its own (non-blocking) HIP stream
+        blocks = _synth_blocks(ca, sdrhip, nstreams, npairs, nblk, 777)
+        A = sdrhip.DeviceArray
+        d_taps = {k: A.from_numpy(ca, v) for k, v in taps.items()}
+        t = sdrhip.StereoTaps(d_taps["rf"].ptr, 101, d_taps["audio"].ptr, len(taps["audio"]), d_taps["pilot"].ptr,
+                              d_taps["stereo"].ptr, 101)
+        st0 = _stereo_state0()
+        d_st = {k: A.from_numpy(ca, np.tile(v, nstreams)) for k, v in st0.items() if k != "prev"}
+        d_pi = A.from_numpy(ca, np.zeros(nstreams, np.float32))
+        d_pq = A.from_numpy(ca, np.zeros(nstreams, np.float32))
+        state = sdrhip.StereoState(d_st["i"].ptr, d_st["q"].ptr, 100, d_pi.ptr, d_pq.ptr, d_st["delay"].ptr, 50,
+                                   d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr,
+                                   d_st["stereo"].ptr, 100, d_st["pll"].ptr)
+        pcm = [A(ca, nstreams * 2 * na * 2) for _ in range(nblk)]
+        works = [ca.stereo_work(D, npairs, up, down, nstreams) for _ in range(2)]
+        ev_f = [sdrhip.Event(ca) for _ in range(2)]
+        ev_b = [sdrhip.Event(ca) for _ in range(2)]
+
+        def run(b0, k):
+            for j in range(k):
+                b, slot = b0 + j, (b0 + j) % 2
+                if j >= 2:
+                    ev_b[slot].wait(ca)
+                ca.stereo_front_u8_dev(blocks[b][0], 2 * npairs, t, state, works[slot])
+                ev_f[slot].record(ca)
+                ev_f[slot].wait(cb)
+                cb.stereo_back_dev(audio_fs, t, state, works[slot], pcm[b], 2 * na)
+                ev_b[slot].record(cb)
+            ev_b[(b0 + k - 1) % 2].wait(ca)
+
+        try:
+            run(0, 1)  # sizes both contexts' scratch (no allocation may happen inside a capture)
+            ca.synchronize()
+            if graph:
+                g = ca.capture(lambda: run(1, nblk - 1))
+                g.launch()
+            else:
+                run(1, nblk - 1)
+            ca.synchronize()
+            cb.synchronize()
+            if graph:
+                g.close()
+            ost = [_stereo_state0() for _ in range(nstreams)]
+            for b in range(nblk):
+                got = pcm[b].download(np.int16).reshape(nstreams, 2 * na)
+                want = _pmap(lambda s: oracle.stereo(D, blocks[b][1][s], taps["rf"], ost[s], up, down,
+                                                     taps["audio"], taps["pilot"], taps["stereo"], audio_fs),
+                             range(nstreams))
+                bad = [s for s in range(nstreams) if not np.array_equal(got[s], want[s])]
+                assert not bad, f"PCM of {len(bad)} streams differs in block {b} (first {bad[:8]})"
+            for k in ("pll", "pilot", "stereo", "stereo_lp", "audio", "delay", "i", "q"):
+                assert_bits(d_st[k].download().reshape(nstreams, -1), np.stack([o[k] for o in ost]), k)
+            assert_bits(np.stack([d_pi.download(), d_pq.download()], axis=1), np.stack([o["prev"] for o in ost]),
+                        "prev")
+        finally:
+            for w in works:
+                w.close()
+            for e in ev_f + ev_b:
+                e.close()
