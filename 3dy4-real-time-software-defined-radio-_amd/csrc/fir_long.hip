@@ -223,12 +223,10 @@ struct LongHArgs {
   int img;    // image halves (multiple of 8)
 };
 
-// VTAP = 1 (A/B, SDR_F16_VTAP=1): the tap-pair table is staged in LDS after the
-// image and each pass's 32 pairs are read into VGPRs by 8 wave-uniform
-// (broadcast) ds_read_b128, so every v_dot2_f32_f16 has VGPR operands only.
-// VTAP = 0: the pairs are SGPR operands of the dot2 (one scalar batch per
-// pass), which halves the dot2 issue rate -- still the faster.
-template <int VTAP>
+// The tap pairs are SGPR operands of the dot2 (one scalar batch per pass).
+// (VGPR pairs read from LDS by broadcast ds_read_b128 were slower: 0.0544 vs
+// 0.0425 ms, profiles/r04a/ab_vtap.txt -- 8 reads per pass on top of the
+// inputs' 10 saturate the LDS at 16 waves per CU.)
 __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t imgw[];  // image as packed pairs
   constexpr int R = kLongRH, NTH = 64 * kLongNW, KP = 32;  // KP tap pairs (d values) per pass
@@ -255,13 +253,6 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
       }
     }
   }
-  // the tap-pair table behind the image (a.img halves = a.img / 2 words)
-  uint32_t* hpl = imgw + (a.img >> 1);
-  const int npairs = (a.ntaps + 1 + 31) / 32 * 32;
-  if constexpr (VTAP) {
-    for (int c = tid; c < (npairs >> 2); c += NTH)
-      *reinterpret_cast<uint4*>(hpl + 4 * c) = *reinterpret_cast<const uint4*>(a.hp2 + 4 * c);
-  }
   __syncthreads();
 
   // output r of this lane: image half index i_r = I0 + r, I0 = lb + halo
@@ -275,21 +266,10 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
   const int npass = (a.ntaps + 1 + KP - 1) / KP;  // d = 0..T
   for (int P = 0; P < npass; ++P) {
     uint32_t hs[KP];
-    if constexpr (VTAP) {
 #pragma unroll
-      for (int i = 0; i < KP; i += 4) {
-        const uint4 t = *reinterpret_cast<const uint4*>(hpl + P * KP + i);
-        hs[i] = t.x;
-        hs[i + 1] = t.y;
-        hs[i + 2] = t.z;
-        hs[i + 3] = t.w;
-      }
-    } else {
+    for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
 #pragma unroll
-      for (int i = 0; i < KP; ++i) hs[i] = hc[P * KP + i];
-#pragma unroll
-      for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
-    }
+    for (int i = 0; i < KP; ++i) asm volatile("" : "+s"(hs[i]));
     // pair W for (r, d): 2W = I0 + r - d, d = KP*P + dd.  Word index
     // W = I0/2 - KP*P/2 + (r - dd)/2 ranges over base + [-(KP/2), 1].
     const int wbase = (I0 >> 1) - (KP / 2) * P - (KP / 2);  // word of relative index 0
@@ -343,8 +323,9 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // eight copies of the reversed f16 taps, copy q shifted by q halves.
 // Same operands as the dot2 kernel (fp16 x, state and taps), fp32
 // accumulation inside the MFMA: the same tolerance contract.
-// default on once measured on the GPU (SDR_F16_MFMA=1 forces it)
-constexpr int kF16MfmaDefault = 0;
+// the default: cfg5h 0.0161-0.0163 vs 0.0427-0.0428 ms on the dot2 kernel
+// (profiles/r04e/ab.txt); SDR_F16_MFMA=0 selects v_dot2
+constexpr int kF16MfmaDefault = 1;
 constexpr int kMfNT = 2;                      // 1,024-output tiles per wave
 constexpr int kMfWaves = 4;                   // one wave per SIMD
 constexpr int kMfOut = 1024 * kMfNT * kMfWaves;  // outputs per workgroup
@@ -540,15 +521,7 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
   a.img = a.halo + OUT_WG + 8;
   const long long blocks = (long long)a.tiles_per_stream * nstreams;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  // SDR_F16_VTAP=1: VGPR tap pairs from LDS (A/B; read per launch).  Not the
-  // default: 0.0544 vs 0.0425 ms on cfg5h (profiles/r04a/ab_vtap.txt) -- the
-  // 8 broadcast ds_read_b128 per pass cost 4 LDS cycles per wave each, which
-  // with the 10 input reads puts 16 waves per CU past the LDS array's rate.
-  if (env_int("SDR_F16_VTAP", 0) != 0)
-    hipLaunchKernelGGL(fir_long_h<1>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2 + (size_t)len * 4,
-                       st, a);
-  else
-    hipLaunchKernelGGL(fir_long_h<0>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2, st, a);
+  hipLaunchKernelGGL(fir_long_h, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * 2, st, a);
   e = hipGetLastError();
   if (e != hipSuccess || ns <= 0) return e;
   hipLaunchKernelGGL(long_commit_h, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st,

@@ -1080,59 +1080,22 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
 // One channel of a lane's window: acc[r] = sum_k h[k] * w[HALO + D r - k] in
 // the reference's order (k ascending, product and sum rounded separately),
 // taps as SGPR operands in NPASS passes -- fir_tile's scan, one channel.
-// VT = 1: the pass's taps are VGPRs, fetched by wave-uniform vector loads
-// (one 16-B request per 4 taps, L1/L2 hits), so every multiply is an
-// all-VGPR v_mul_f32 -- an SGPR operand halves the VALU rate (4.2 vs 2.2
-// cycles per instruction per SIMD, profiles/r02_ubench_valu.txt).  The
-// bits are the same: only where the tap value comes from changes.
-template <int D, int T, int R, bool FMA, int VT = 0, int NP = SDR_NPASS>
+template <int D, int T, int R, bool FMA>
 __device__ __forceinline__ void scan_one(const float* w, float (&acc)[R], const float* h) {
   using G = Geom<D, T, R, true, 1>;
-  // VT: passes of a multiple of 4 taps, so each pass's taps are 16-B loads
-  constexpr int NPASS = NP, KP0 = (T + NPASS - 1) / NPASS, KP = VT ? (KP0 + 3) / 4 * 4 : KP0;
-  constexpr int KP4 = (KP + 3) / 4 * 4;
+  constexpr int NPASS = SDR_NPASS, KP = (T + NPASS - 1) / NPASS;
   using hconst = const __attribute__((address_space(4))) float*;
   const hconst hc = (hconst)h;
-  using gconst = const __attribute__((address_space(1))) float*;
-  gconst hv = (gconst)h;
-  if constexpr (VT) {
-    // launder the (uniform) tap pointer into a VGPR: the compiler then emits
-    // global vector loads, whose results stay in VGPRs
-    uintptr_t hp = reinterpret_cast<uintptr_t>(h);
-    asm volatile("" : "+v"(hp));
-    hv = (gconst)hp;
-  }
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-  float hs[KP4];
+  float hs[KP];
   static_for<0, NPASS>([&](auto pi) {
     constexpr int k0 = decltype(pi)::value * KP;
     constexpr int k1 = k0 + KP < T ? k0 + KP : T;
-    if constexpr (VT) {
-      // taps k0 .. k1 - 1 (k0 % 4 == 0, h 16-B aligned: checked at dispatch);
-      // the last pass's ragged end by dword loads, never past T
-      if constexpr (k0 % 4 == 0) {
 #pragma unroll
-        for (int i = 0; i + 4 <= k1 - k0; i += 4) {
-          typedef const __attribute__((address_space(1))) nf4* g4;
-          const nf4 t = *(g4)(hv + k0 + i);
-          hs[i] = t.x;
-          hs[i + 1] = t.y;
-          hs[i + 2] = t.z;
-          hs[i + 3] = t.w;
-        }
+    for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
 #pragma unroll
-        for (int i = (k1 - k0) / 4 * 4; i < k1 - k0; ++i) hs[i] = hv[k0 + i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < k1 - k0; ++i) hs[i] = hv[k0 + i];
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
-#pragma unroll
-      for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
-    }
+    for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
     constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
     constexpr int whi = G::HALO + D * (R - 1) - k0;
     constexpr int clo = wlo / 4, chi = whi / 4;
@@ -1173,10 +1136,7 @@ __device__ __forceinline__ void scan_one(const float* w, float (&acc)[R], const 
 // workgroup lives about as long as one channel's scan instead of two, with
 // half the staging registers per wave.  Same tiles, arithmetic, order,
 // outputs and state as fir_tile (src/filter.cpp:123-140, 85-102).
-#ifndef SDR_VT_NPASS
-#define SDR_VT_NPASS 3
-#endif
-template <int D, int T, int R, Src SRC, bool FMA = false, int VT = 0>
+template <int D, int T, int R, Src SRC, bool FMA = false>
 __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __restrict__ h) {
   constexpr int NW = 1, NTH = 64;
   constexpr bool DEMOD = true;
@@ -1243,7 +1203,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = lds[lbase + r];
   } else {
-    scan_one<D, T, R, FMA, VT, VT ? SDR_VT_NPASS : SDR_NPASS>(lds + lbase, acc, h);
+    scan_one<D, T, R, FMA>(lds + lbase, acc, h);
   }
   if (c == 1) {
 #pragma unroll
@@ -1468,7 +1428,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
 }
 
 // fir_tile_sc launch: one two-wave workgroup per tile, XCD slabs
-template <int D, int T, int R, Src SRC, bool FMA = false, int VT = 0>
+template <int D, int T, int R, Src SRC, bool FMA = false>
 hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
   using G = Geom<D, T, R, true, 1>;
   FirLaunch a = a0;
@@ -1480,7 +1440,7 @@ hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
   a.ablate = ablate;
   const long long per_xcd = (total + 7) / 8;
   const size_t lds = (size_t)(2 * G::LDS_LEN + 64 * R) * sizeof(float);
-  hipLaunchKernelGGL((fir_tile_sc<D, T, R, SRC, FMA, VT>), dim3((unsigned)(8 * per_xcd)), dim3(128), lds, st, a, h);
+  hipLaunchKernelGGL((fir_tile_sc<D, T, R, SRC, FMA>), dim3((unsigned)(8 * per_xcd)), dim3(128), lds, st, a, h);
   return hipGetLastError();
 }
 
@@ -1497,13 +1457,6 @@ bool sc_enabled() {
 bool sc_u8_enabled() {
   const char* e = std::getenv("SDR_FIR_SC_U8");
   return !e || std::atoi(e) != 0;
-}
-
-// fir_tile_sc's taps as VGPRs (SDR_FIR_VTAP_U8 / SDR_FIR_VTAP, read per
-// launch so a test runs both); see scan_one
-bool sc_vtap(Src src) {
-  const char* e = std::getenv(src == Src::U8 ? "SDR_FIR_VTAP_U8" : "SDR_FIR_VTAP");
-  return e && std::atoi(e) != 0;
 }
 
 // Tile shape per decimation factor: R outputs per lane, one wave per
@@ -1547,12 +1500,8 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
         // fir_tile_sc by default (SDR_FIR_SC=0 / SDR_FIR_SC_U8=0: fir_tile,
         // the u8 wire format on persistent groups) -- DESIGN.md 4.1, 5.2
         case 10:
-          if (SRC == Src::F32 ? sc_enabled() : sc_u8_enabled()) {
-            if (sc_vtap(SRC) && (reinterpret_cast<uintptr_t>(h) & 15) == 0)
-              return a.fma ? run_tile_sc<10, 101, 2, SRC, true, 1>(a, h, st)
-                           : run_tile_sc<10, 101, 2, SRC, false, 1>(a, h, st);
+          if (SRC == Src::F32 ? sc_enabled() : sc_u8_enabled())
             return a.fma ? run_tile_sc<10, 101, 2, SRC, true>(a, h, st) : run_tile_sc<10, 101, 2, SRC>(a, h, st);
-          }
           return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 64)
                        : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1>(a, h, st, kPersistFused, 64);
         case 5:

@@ -108,7 +108,7 @@ def parse(argv=None):
     ap.add_argument("--batches", type=int, default=2, help="distinct input batches the steps cycle over")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per replayed HIP graph")
     ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
-    ap.add_argument("--stereo-pipeline", type=int, default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "0")),
+    ap.add_argument("--stereo-pipeline", type=int, default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "1")),
                     help="stereo configs: 1 = each step as two stages on two contexts' streams (front end + band-pass "
                          "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
