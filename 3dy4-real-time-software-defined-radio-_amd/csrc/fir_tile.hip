@@ -725,14 +725,28 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SDR_FIR_LB
 #define SDR_FIR_LB 1024
 #endif
+// TM = 2 (round 4): the T taps live in VGPRs for the whole launch, loaded
+// once per persistent wave.  Every multiply is then an all-VGPR v_mul_f32,
+// which issues at twice the rate of one with an SGPR operand (2.2 vs 4.2
+// cycles per instruction per SIMD, profiles/r02_ubench_valu.txt); the cost
+// is T registers per lane, i.e. three waves per SIMD (<= 168 VGPRs) instead
+// of four -- the mul+add issue rate at three waves (2.24 cycles) is the best
+// measured.  The wave-uniform per-tile tap loads of the round-4 fir_tile_sc
+// VGPR variant (26 vector loads per pass per tile) are gone: a persistent
+// wave loads its taps once.
+constexpr int kVtWaves = 12;  // TM 2: 3 waves per SIMD
+#ifndef SDR_VT_PF
+#define SDR_VT_PF 2
+#endif
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
-__global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const float* __restrict__ h) {
+__global__ __launch_bounds__(TM == 2 ? 64 * kVtWaves : SDR_FIR_LB) void fir_tile_grp(FirLaunch a,
+                                                                                      const float* __restrict__ h) {
   using G = Geom<D, T, R, DEMOD, NW>;
   constexpr int NTH = G::NTH;
   static_assert(NW == 1, "one wave per tile");
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
   static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
-  static_assert(TM == 1, "taps as SGPR operands");
+  static_assert(TM == 1 || TM == 2, "taps as SGPR operands (1) or VGPRs (2)");
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int next_tile;  // the group's claim counter
@@ -767,6 +781,17 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
   };
   const int first = claim();
   if (first < 0) return;
+  // TM 2: the taps, once per wave (scalar loads, then one move each into a
+  // VGPR that the asm pins there for the launch)
+  float hv[TM == 2 ? T : 1];
+  if constexpr (TM == 2) {
+    using hconst = const __attribute__((address_space(4))) float*;
+    const hconst hc = (hconst)h;
+#pragma unroll
+    for (int k = 0; k < T; ++k) hv[k] = hc[k];
+#pragma unroll
+    for (int k = 0; k < T; ++k) asm volatile("" : "+v"(hv[k]));
+  }
 #ifdef SDR_FIR_TRACE
   unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime(), tr_m0 = __builtin_amdgcn_s_memtime();
 #define SDR_TRACE_AT(i)                                        \
@@ -877,6 +902,53 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     if (a.ablate == 2) {
       acc0[0] = lds0[lbase];
       acc1[0] = lds1[lbase];
+    } else if constexpr (TM == 2) {
+      // one pass over all T taps (VGPRs): chunks of the lane's window from
+      // the newest down, so every output visits k = 0..T-1 in order
+      const float* w0 = lds0 + lbase;
+      const float* w1 = lds1 + lbase;
+      // SDR_VT_PF chunks of LDS reads in flight ahead of the one multiplied
+      constexpr int chi = (G::HALO + D * (R - 1)) / 4;
+      constexpr int clo = (G::HALO - (T - 1)) / 4;
+      constexpr int PF = SDR_VT_PF;
+      float4 b0[PF + 1], b1[PF + 1];
+      static_for<0, PF>([&](auto pi) {
+        constexpr int c = chi - decltype(pi)::value;
+        if constexpr (c >= clo) {
+          b0[pi] = *reinterpret_cast<const float4*>(w0 + 4 * c);
+          if (NCH == 2) b1[pi] = *reinterpret_cast<const float4*>(w1 + 4 * c);
+        }
+      });
+      static_for<0, chi - clo + 1>([&](auto ci) {
+        constexpr int c = chi - decltype(ci)::value;
+        constexpr int cur = decltype(ci)::value % (PF + 1), nxt = (decltype(ci)::value + PF) % (PF + 1);
+        if constexpr (c - PF >= clo) {
+          b0[nxt] = *reinterpret_cast<const float4*>(w0 + 4 * (c - PF));
+          if (NCH == 2) b1[nxt] = *reinterpret_cast<const float4*>(w1 + 4 * (c - PF));
+        }
+        const float4 q0 = b0[cur], q1 = NCH == 2 ? b1[cur] : b0[cur];
+        const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
+        const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
+        static_for<0, 4>([&](auto ji) {
+          constexpr int j = 3 - decltype(ji)::value;
+          static_for<0, R>([&](auto ri) {
+            constexpr int r = decltype(ri)::value;
+            constexpr int k = G::HALO + D * r - (4 * c + j);
+            if constexpr (k >= 0 && k < T) {
+              if constexpr (FMA) {
+                acc0[r] = __builtin_fmaf(hv[k], e0[j], acc0[r]);
+                if (NCH == 2) acc1[r] = __builtin_fmaf(hv[k], e1[j], acc1[r]);
+              } else {
+                acc0[r] = acc0[r] + hv[k] * e0[j];
+                if (NCH == 2) acc1[r] = acc1[r] + hv[k] * e1[j];
+              }
+            }
+          });
+        });
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
+        __builtin_amdgcn_sched_barrier(0);
+      });
     } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
@@ -1377,15 +1449,18 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   a.ablate = ablate;
   static const int persist_env = env_int("SDR_FIR_PERSIST", -1);  // A/B
   if (persist_env >= 0) persist = persist_env != 0;
-  if (persist) {
+  if (TM == 2 || persist) {  // VGPR taps: persistent groups only
     // a CU's LDS (160 KiB on gfx950, read from the device), less the claim counter
     const long long kLds = (long long)device_lds_bytes() - 64;
     constexpr long long slice = (long long)G::SMEM * sizeof(float);
     if (kLds < slice) return hipErrorInvalidConfiguration;
     static const int wpg_env = env_int("SDR_FIR_WPG", 0);  // timing experiments
-    long long wpg = std::min<long long>(16, kLds / slice);
+    // waves per CU: 16 (4 per SIMD at <= 128 VGPRs), TM 2: kVtWaves (3 per SIMD)
+    constexpr long long kWaveCap = TM == 2 ? kVtWaves : 16;
+    long long wpg = std::min<long long>(kWaveCap, kLds / slice);
     if (wpg_env > 0) wpg = std::min<long long>(wpg, wpg_env);
-    const long long wg_per_cu = std::max<long long>(1, std::min<long long>(32 / wpg, kLds / (wpg * slice)));
+    const long long wg_per_cu =
+        std::max<long long>(1, std::min<long long>(TM == 2 ? kVtWaves / wpg : 32 / wpg, kLds / (wpg * slice)));
     long long groups = std::min<long long>(ncu * wg_per_cu, (total + wpg - 1) / wpg);
     // timing experiments: about k tiles per wave, as many groups as that takes
     static const int wave_tiles = env_int("SDR_FIR_WAVE_TILES", 0);
@@ -1422,8 +1497,9 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
     blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
   }
   const size_t lds = (size_t)G::SMEM * sizeof(float);
-  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st,
-                     a, h);
+  if constexpr (TM == 1)
+    hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds,
+                       st, a, h);
   return hipGetLastError();
 }
 
@@ -1456,6 +1532,14 @@ bool sc_enabled() {
 // fir_tile_grp (read per launch, so a test runs both)
 bool sc_u8_enabled() {
   const char* e = std::getenv("SDR_FIR_SC_U8");
+  return !e || std::atoi(e) != 0;
+}
+
+// the u8 wire path (D = 10) on fir_tile_grp with VGPR taps (TM 2);
+// SDR_FIR_VT_U8=0 selects the SGPR-tap kernels above (read per launch, so a
+// test runs both)
+bool vt_u8_enabled() {
+  const char* e = std::getenv("SDR_FIR_VT_U8");
   return !e || std::atoi(e) != 0;
 }
 
@@ -1500,6 +1584,12 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
         // fir_tile_sc by default (SDR_FIR_SC=0 / SDR_FIR_SC_U8=0: fir_tile,
         // the u8 wire format on persistent groups) -- DESIGN.md 4.1, 5.2
         case 10:
+          // u8 wire format: persistent groups with VGPR taps (SDR_FIR_VT_U8=0:
+          // the split-channel kernel)
+          if constexpr (SRC == Src::U8)
+            if (vt_u8_enabled())
+              return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 2, true>(a, h, st, true, 64)
+                           : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 2>(a, h, st, true, 64);
           if (SRC == Src::F32 ? sc_enabled() : sc_u8_enabled())
             return a.fma ? run_tile_sc<10, 101, 2, SRC, true>(a, h, st) : run_tile_sc<10, 101, 2, SRC>(a, h, st);
           return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 64)

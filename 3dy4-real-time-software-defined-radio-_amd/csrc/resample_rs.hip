@@ -307,6 +307,12 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
 // amount to every lane), so build_lanes() sorts the items by that class and
 // deals them round-robin over the 28 groups: a group gets two items of one
 // class only when the class has more than 28 items.
+#ifndef SDR_LP_ORD
+#define SDR_LP_ORD 0
+#endif
+#ifndef SDR_LP_EARLY
+#define SDR_LP_EARLY 0
+#endif
 constexpr int kLpWaves = 7;
 constexpr int kLpSlots = 64 * kLpWaves;
 constexpr int kLpGroups = kLpSlots / 16;
@@ -421,7 +427,7 @@ __global__ __launch_bounds__(kLpSlots) void build_lp_tables(const float* __restr
 // or past the end.
 // The staging threads: tid of nth, in waves wv of nwv (all of the compute
 // waves, or the one loader wave).
-template <int CMAX>
+template <int CMAX, bool DMA_FIRST = false>
 __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, int tid, int nth, int wv, int nwv,
                                          int ln) {
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
@@ -449,13 +455,21 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
     }
     *reinterpret_cast<float4*>(buf + 4 * j) = make_float4(w4[0], w4[1], w4[2], w4[3]);
   };
+  auto dma = [&]() __attribute__((always_inline)) {
+    // lanes of one instruction are consecutive chunks
+    for (int j0 = (int)(jlo & ~63LL) + wv * 64; j0 < jhi; j0 += 64 * nwv) {
+      const int j = j0 + ln;
+      if (j >= jlo && j < jhi) __builtin_amdgcn_global_load_lds(xs + P0 + 4LL * j, buf + 4 * j0, 16, 0, 0);
+    }
+  };
+  // DMA_FIRST (the loader wave, which waits for nothing else): the span's
+  // DMAs go out before the edge loads, whose waits then cover the DMAs too
+  // but no longer hold back their issue by a memory latency on every
+  // stream's first item
+  if constexpr (DMA_FIRST) dma();
   for (int j = tid; j < (int)jlo && j < nch; j += nth) edge(j);
   for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += nth) edge(j);
-  // DMA: lanes of one instruction are consecutive chunks
-  for (int j0 = (int)(jlo & ~63LL) + wv * 64; j0 < jhi; j0 += 64 * nwv) {
-    const int j = j0 + ln;
-    if (j >= jlo && j < jhi) __builtin_amdgcn_global_load_lds(xs + P0 + 4LL * j, buf + 4 * j0, 16, 0, 0);
-  }
+  if constexpr (!DMA_FIRST) dma();
 }
 
 template <int CMAX, int K, int LW, int NOLDS = 0>
@@ -510,11 +524,36 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
       // shifted tap is 0 and the input is replaced by 0 (term +0: acc unchanged)
       const bool edge = (cc == 0) || (u >= CMAX);
       const bool ok = !edge || (u + A - 3 >= 0 && u + A - 3 < CMAX);
+      if constexpr (SDR_LP_ORD && K == 7) {
+        // the K products first, then the K sums: every add reads a product
+        // made K instructions earlier (a mul and the add that consumes it
+        // issued back to back cost one wave 6.3 instead of 4.5 cycles per
+        // instruction, profiles/r02_ubench_valu.txt "mul vv + add").  Same
+        // operations, same order per output.
+        float v[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float v = cur[k][jj];
-        if (edge) v = ok ? v : 0.0f;
-        acc[k] = acc[k] + tp[u] * v;
+        for (int k = 0; k < K; ++k) {
+          v[k] = cur[k][jj];
+          if (edge) v[k] = ok ? v[k] : 0.0f;
+        }
+        float t0, t1, t2, t3, t4, t5, t6;
+        asm volatile(
+            "v_mul_f32 %7, %14, %15\n\tv_mul_f32 %8, %14, %16\n\tv_mul_f32 %9, %14, %17\n\t"
+            "v_mul_f32 %10, %14, %18\n\tv_mul_f32 %11, %14, %19\n\tv_mul_f32 %12, %14, %20\n\t"
+            "v_mul_f32 %13, %14, %21\n\t"
+            "v_add_f32 %0, %0, %7\n\tv_add_f32 %1, %1, %8\n\tv_add_f32 %2, %2, %9\n\t"
+            "v_add_f32 %3, %3, %10\n\tv_add_f32 %4, %4, %11\n\tv_add_f32 %5, %5, %12\n\t"
+            "v_add_f32 %6, %6, %13"
+            : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+              "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6)
+            : "v"(tp[u]), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]));
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          float v = cur[k][jj];
+          if (edge) v = ok ? v : 0.0f;
+          acc[k] = acc[k] + tp[u] * v;
+        }
       }
     }
 #pragma unroll
@@ -559,7 +598,7 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     if (!LW)
       lp_stage<CMAX>(a, buf, it, threadIdx.x, kLpSlots, wv, kLpWaves, ln);
     else if (loader)
-      lp_stage<CMAX>(a, buf, it, ln, 64, 0, 1, ln);
+      lp_stage<CMAX, SDR_LP_EARLY != 0>(a, buf, it, ln, 64, 0, 1, ln);
   };
   // the first item's DMA runs while this lane's item and taps are loaded
   stage(bufA, i0);
@@ -592,6 +631,10 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     // (its own edge loads read the old state, before this); else it is
     // brought into LDS by DMA during the compute and stored after it.
     const bool commit = it % a.nbat == 0;
+    const bool odd = ((it - i0) & 1) != 0;
+    // SDR_LP_EARLY (loader wave): the next item's DMAs before this item's
+    // state copy, whose load-to-store wait would otherwise hold them back
+    if (SDR_LP_EARLY && LW && it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
     if (LW) {
       if (loader && commit) {
         const long long s = it / a.nbat;
@@ -601,8 +644,7 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
       __builtin_amdgcn_global_load_lds(a.x + (long long)(it / a.nbat) * a.x_stride + (a.n - a.ns) + threadIdx.x,
                                        cbuf + wv * 64, 4, 0, 0);
     }
-    const bool odd = ((it - i0) & 1) != 0;
-    if (it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
+    if (!(SDR_LP_EARLY && LW) && it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
     if (a.ablate != 2 && !loader) {
       if (odd)
         lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
