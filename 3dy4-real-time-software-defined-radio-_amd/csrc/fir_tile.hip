@@ -1535,12 +1535,13 @@ bool sc_u8_enabled() {
   return !e || std::atoi(e) != 0;
 }
 
-// the u8 wire path (D = 10) on fir_tile_grp with VGPR taps (TM 2);
-// SDR_FIR_VT_U8=0 selects the SGPR-tap kernels above (read per launch, so a
-// test runs both)
+// the u8 wire path (D = 10) on fir_tile_grp with VGPR taps (TM 2), opt-in
+// (SDR_FIR_VT_U8=1): 0.0845 vs 0.0814 ms on cfg2u8, scan-only 72.5 vs 73.9 us
+// (profiles/r04f/) -- the taps' location does not bound the scan (read per
+// launch, so a test runs both)
 bool vt_u8_enabled() {
   const char* e = std::getenv("SDR_FIR_VT_U8");
-  return !e || std::atoi(e) != 0;
+  return e && std::atoi(e) != 0;
 }
 
 // Tile shape per decimation factor: R outputs per lane, one wave per

@@ -307,11 +307,14 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
 // amount to every lane), so build_lanes() sorts the items by that class and
 // deals them round-robin over the 28 groups: a group gets two items of one
 // class only when the class has more than 28 items.
-#ifndef SDR_LP_ORD
-#define SDR_LP_ORD 0
-#endif
+// SDR_LP_EARLY: the loader wave issues the next item's DMAs before the edge
+// loads and the state copy (0.1207-0.1211 vs 0.1206-0.1236 ms on cfg3, same
+// box, profiles/r04f/ab_resample_loader.txt).  The ordered scan (the K
+// products, then the K sums, inline asm) made the scan alone 5 % faster
+// (0.1018 vs 0.1072 ms without staging) and the kernel 3 % slower
+// (profiles/r04f/ab_resample_ord.txt); not kept.
 #ifndef SDR_LP_EARLY
-#define SDR_LP_EARLY 0
+#define SDR_LP_EARLY 1
 #endif
 constexpr int kLpWaves = 7;
 constexpr int kLpSlots = 64 * kLpWaves;
@@ -524,36 +527,11 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
       // shifted tap is 0 and the input is replaced by 0 (term +0: acc unchanged)
       const bool edge = (cc == 0) || (u >= CMAX);
       const bool ok = !edge || (u + A - 3 >= 0 && u + A - 3 < CMAX);
-      if constexpr (SDR_LP_ORD && K == 7) {
-        // the K products first, then the K sums: every add reads a product
-        // made K instructions earlier (a mul and the add that consumes it
-        // issued back to back cost one wave 6.3 instead of 4.5 cycles per
-        // instruction, profiles/r02_ubench_valu.txt "mul vv + add").  Same
-        // operations, same order per output.
-        float v[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          v[k] = cur[k][jj];
-          if (edge) v[k] = ok ? v[k] : 0.0f;
-        }
-        float t0, t1, t2, t3, t4, t5, t6;
-        asm volatile(
-            "v_mul_f32 %7, %14, %15\n\tv_mul_f32 %8, %14, %16\n\tv_mul_f32 %9, %14, %17\n\t"
-            "v_mul_f32 %10, %14, %18\n\tv_mul_f32 %11, %14, %19\n\tv_mul_f32 %12, %14, %20\n\t"
-            "v_mul_f32 %13, %14, %21\n\t"
-            "v_add_f32 %0, %0, %7\n\tv_add_f32 %1, %1, %8\n\tv_add_f32 %2, %2, %9\n\t"
-            "v_add_f32 %3, %3, %10\n\tv_add_f32 %4, %4, %11\n\tv_add_f32 %5, %5, %12\n\t"
-            "v_add_f32 %6, %6, %13"
-            : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
-              "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6)
-            : "v"(tp[u]), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]));
-      } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float v = cur[k][jj];
-          if (edge) v = ok ? v : 0.0f;
-          acc[k] = acc[k] + tp[u] * v;
-        }
+      for (int k = 0; k < K; ++k) {
+        float v = cur[k][jj];
+        if (edge) v = ok ? v : 0.0f;
+        acc[k] = acc[k] + tp[u] * v;
       }
     }
 #pragma unroll
