@@ -725,28 +725,14 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SDR_FIR_LB
 #define SDR_FIR_LB 1024
 #endif
-// TM = 2 (round 4): the T taps live in VGPRs for the whole launch, loaded
-// once per persistent wave.  Every multiply is then an all-VGPR v_mul_f32,
-// which issues at twice the rate of one with an SGPR operand (2.2 vs 4.2
-// cycles per instruction per SIMD, profiles/r02_ubench_valu.txt); the cost
-// is T registers per lane, i.e. three waves per SIMD (<= 168 VGPRs) instead
-// of four -- the mul+add issue rate at three waves (2.24 cycles) is the best
-// measured.  The wave-uniform per-tile tap loads of the round-4 fir_tile_sc
-// VGPR variant (26 vector loads per pass per tile) are gone: a persistent
-// wave loads its taps once.
-constexpr int kVtWaves = 12;  // TM 2: 3 waves per SIMD
-#ifndef SDR_VT_PF
-#define SDR_VT_PF 2
-#endif
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
-__global__ __launch_bounds__(TM == 2 ? 64 * kVtWaves : SDR_FIR_LB) void fir_tile_grp(FirLaunch a,
-                                                                                      const float* __restrict__ h) {
+__global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const float* __restrict__ h) {
   using G = Geom<D, T, R, DEMOD, NW>;
   constexpr int NTH = G::NTH;
   static_assert(NW == 1, "one wave per tile");
   static_assert(NCH == 2 || !DEMOD, "the discriminator needs I and Q");
   static_assert(SRC == Src::F32 || NCH == 2, "u8 wire format carries I and Q");
-  static_assert(TM == 1 || TM == 2, "taps as SGPR operands (1) or VGPRs (2)");
+  static_assert(TM == 1, "taps as SGPR operands");
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int next_tile;  // the group's claim counter
@@ -781,17 +767,6 @@ __global__ __launch_bounds__(TM == 2 ? 64 * kVtWaves : SDR_FIR_LB) void fir_tile
   };
   const int first = claim();
   if (first < 0) return;
-  // TM 2: the taps, once per wave (scalar loads, then one move each into a
-  // VGPR that the asm pins there for the launch)
-  float hv[TM == 2 ? T : 1];
-  if constexpr (TM == 2) {
-    using hconst = const __attribute__((address_space(4))) float*;
-    const hconst hc = (hconst)h;
-#pragma unroll
-    for (int k = 0; k < T; ++k) hv[k] = hc[k];
-#pragma unroll
-    for (int k = 0; k < T; ++k) asm volatile("" : "+v"(hv[k]));
-  }
 #ifdef SDR_FIR_TRACE
   unsigned long long tr_sum[4] = {}, tr_last = 0, tr_n = 0, tr_r0 = __builtin_amdgcn_s_memrealtime(), tr_m0 = __builtin_amdgcn_s_memtime();
 #define SDR_TRACE_AT(i)                                        \
@@ -902,53 +877,6 @@ __global__ __launch_bounds__(TM == 2 ? 64 * kVtWaves : SDR_FIR_LB) void fir_tile
     if (a.ablate == 2) {
       acc0[0] = lds0[lbase];
       acc1[0] = lds1[lbase];
-    } else if constexpr (TM == 2) {
-      // one pass over all T taps (VGPRs): chunks of the lane's window from
-      // the newest down, so every output visits k = 0..T-1 in order
-      const float* w0 = lds0 + lbase;
-      const float* w1 = lds1 + lbase;
-      // SDR_VT_PF chunks of LDS reads in flight ahead of the one multiplied
-      constexpr int chi = (G::HALO + D * (R - 1)) / 4;
-      constexpr int clo = (G::HALO - (T - 1)) / 4;
-      constexpr int PF = SDR_VT_PF;
-      float4 b0[PF + 1], b1[PF + 1];
-      static_for<0, PF>([&](auto pi) {
-        constexpr int c = chi - decltype(pi)::value;
-        if constexpr (c >= clo) {
-          b0[pi] = *reinterpret_cast<const float4*>(w0 + 4 * c);
-          if (NCH == 2) b1[pi] = *reinterpret_cast<const float4*>(w1 + 4 * c);
-        }
-      });
-      static_for<0, chi - clo + 1>([&](auto ci) {
-        constexpr int c = chi - decltype(ci)::value;
-        constexpr int cur = decltype(ci)::value % (PF + 1), nxt = (decltype(ci)::value + PF) % (PF + 1);
-        if constexpr (c - PF >= clo) {
-          b0[nxt] = *reinterpret_cast<const float4*>(w0 + 4 * (c - PF));
-          if (NCH == 2) b1[nxt] = *reinterpret_cast<const float4*>(w1 + 4 * (c - PF));
-        }
-        const float4 q0 = b0[cur], q1 = NCH == 2 ? b1[cur] : b0[cur];
-        const float e0[4] = {q0.x, q0.y, q0.z, q0.w};
-        const float e1[4] = {q1.x, q1.y, q1.z, q1.w};
-        static_for<0, 4>([&](auto ji) {
-          constexpr int j = 3 - decltype(ji)::value;
-          static_for<0, R>([&](auto ri) {
-            constexpr int r = decltype(ri)::value;
-            constexpr int k = G::HALO + D * r - (4 * c + j);
-            if constexpr (k >= 0 && k < T) {
-              if constexpr (FMA) {
-                acc0[r] = __builtin_fmaf(hv[k], e0[j], acc0[r]);
-                if (NCH == 2) acc1[r] = __builtin_fmaf(hv[k], e1[j], acc1[r]);
-              } else {
-                acc0[r] = acc0[r] + hv[k] * e0[j];
-                if (NCH == 2) acc1[r] = acc1[r] + hv[k] * e1[j];
-              }
-            }
-          });
-        });
-#pragma unroll
-        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc0[r]), "+v"(acc1[r]));
-        __builtin_amdgcn_sched_barrier(0);
-      });
     } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
@@ -1359,264 +1287,6 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   }
 }
 
-// ------------------------------------------------- loader-ring front end --
-// fir_ring (round 4, f32 fused front end): one persistent workgroup per CU
-// owns a contiguous run of tiles (cfg2: 208 = four whole streams).  Its last
-// wave is a loader: it streams every tile's I and Q spans into a ring of
-// kRingSlots LDS slots by LDS-DMA (non-temporal), keeping kRingAhead tiles in
-// flight and publishing each slot behind a counted vmcnt; kRingCons consumer
-// waves take the tiles round robin, scan both channels (fir_tile's scan, SGPR
-// taps), run the discriminator, store, and release the slot.  No workgroup
-// is ever dispatched mid-launch (fir_tile_sc's one-tile workgroups kept a CU
-// at 10.6 of 14 resident) and the loads never wait behind
-// arithmetic.  Same tiles, order, outputs and state as fir_tile.
-// Handshake: per slot a FULL word (generation + 1, loader -> consumers) and
-// a FREE word (generation, consumer -> loader) in LDS; tile i of the run
-// uses slot i % kRingSlots in generation i / kRingSlots.  Every spin is
-// bounded (kRingSpin polls with s_sleep): a wave that gives up leaves
-// (its outputs wrong, never a hang).
-constexpr int kRingCons = 8;
-constexpr int kRingLoad = 4;  // loader waves: loader l stages tiles l, l + kRingLoad, ...
-constexpr int kRingSlots = 14;
-constexpr int kRingAhead = 2;  // tiles in flight per loader wave
-constexpr int kRingSpin = 1 << 22;
-// The handshake words are read and written by inline asm on their LDS
-// offsets: to the compiler a plain LDS access after an LDS-DMA may alias the
-// DMA's destination, and its waitcnt pass then drains every DMA in flight
-// (vmcnt(0)) before each poll -- no loads would stay in flight.
-__device__ __forceinline__ unsigned lds_off(const void* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ int lds_peek(unsigned off) {
-  int v;
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(off) : "memory");
-  return __builtin_amdgcn_readfirstlane(v);
-}
-// one 16-B LDS-DMA chunk per lane into lds + 16 * lane (wave-uniform lds)
-__device__ __forceinline__ void ring_dma(const float* g, float* lds) {
-  __builtin_amdgcn_global_load_lds(g, lds, 16, 0, SDR_FIR_NT ? 2 : 0);
-}
-__device__ __forceinline__ void lds_poke(unsigned off, int v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
-}
-
-template <int D, int T, int R, bool FMA>
-__global__ __launch_bounds__(64 * (kRingCons + kRingLoad)) void fir_ring(FirLaunch a, const float* __restrict__ h) {
-  constexpr int NW = 1, NTH = 64, NCH = 2;
-  constexpr bool DEMOD = true;
-  constexpr Src SRC = Src::F32;
-  using G = Geom<D, T, R, DEMOD, NW>;
-  // DMA wave-instructions per channel span (the last one partly masked):
-  // a constant, so vmcnt counts tiles
-  constexpr int NDMA = (G::LDS4 + 63) / 64;
-  static_assert(2 * NDMA * kRingAhead <= 63, "vmcnt counts at most 63 outstanding");
-  static_assert(kRingSlots >= kRingLoad * kRingAhead + 1, "a tile is published before its slot is waited for again");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  int* full_p = reinterpret_cast<int*>(smem + kRingSlots * G::SMEM);
-  const unsigned full = lds_off(full_p), freew = full + 4 * kRingSlots;  // LDS byte offsets
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const long long n = a.n;
-  const long long nout = n / D;
-  const int ns = a.ns;
-  const int total = a.nstreams * a.tiles_per_stream;
-  // the workgroup's k-th tile (a.walk 1: XCD slabs as fir_tile_grp -- the
-  // 32 CUs of an XCD interleave through one contiguous eighth of the tiles,
-  // so the chip streams through a few windows of the input instead of one
-  // per CU, and a tile's halo is its neighbour's tail in the same L2;
-  // a.walk 0: a contiguous run per workgroup)
-  int t0, tstep, cnt;
-  if (a.walk) {
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, gps = gridDim.x >> 3;
-    const int s_lo = x * a.slab, s_hi = min(s_lo + a.slab, total);
-    t0 = s_lo + j;
-    tstep = gps;
-    cnt = t0 < s_hi ? (s_hi - t0 + gps - 1) / gps : 0;
-  } else {
-    t0 = (int)blockIdx.x * a.tiles_per_wg;
-    tstep = 1;
-    cnt = min(a.tiles_per_wg, total - t0);
-  }
-  if (cnt <= 0) return;
-  if (threadIdx.x < 2 * kRingSlots) full_p[threadIdx.x] = 0;
-  __syncthreads();  // the only workgroup barrier
-
-  if (wv >= kRingCons) {
-    // ---------------- loaders: wave kRingCons + l stages tiles l + kRingLoad * q
-    auto issue = [&](int i) __attribute__((always_inline)) {
-      const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, t0 + i * tstep);
-      float* slot = smem + (i % kRingSlots) * G::SMEM;
-      const long long pmax = (n & ~3LL) - 4;  // last whole aligned chunk
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float* x = c ? tr.x1 : tr.x0;
-#pragma unroll
-        for (int r = 0; r < NDMA; ++r) {
-          const int j = r * 64 + lane;
-          long long p = tr.pb + 4LL * j;
-          // chunks outside [0, n): an in-bounds chunk instead (the consumer's
-          // edge fill rewrites what a stored output reads); every
-          // instruction keeps its active lanes, so vmcnt counts tiles
-          p = p < 0 ? 0 : (p > pmax ? pmax : p);
-          if (j < G::LDS4) ring_dma(x + p, slot + c * G::LDS_LEN + 4 * (r * 64));
-        }
-      }
-    };
-    auto publish = [&](int i) __attribute__((always_inline)) {
-      if (lane == 0) lds_poke(full + 4 * (i % kRingSlots), i / kRingSlots + 1);
-    };
-    const int l = wv - kRingCons;
-    int q = 0;
-    for (int i = l; i < cnt; i += kRingLoad, ++q) {
-      if (q >= kRingAhead) {
-        // this loader's tile q - kRingAhead has landed once at most
-        // kRingAhead - 1 of its tiles' DMAs are outstanding
-        static_assert(2 * NDMA * (kRingAhead - 1) == 12, "the vmcnt below counts 1 tile of 12 DMAs");
-        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        publish(i - kRingLoad * kRingAhead);
-      }
-      if (i >= kRingSlots) {
-        int spin = 0;
-        while (lds_peek(freew + 4 * (i % kRingSlots)) != i / kRingSlots) {
-          if (++spin > kRingSpin) return;
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      issue(i);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int i = l + kRingLoad * (q > kRingAhead ? q - kRingAhead : 0); i < cnt; i += kRingLoad) publish(i);
-    return;
-  }
-
-  // ---------------- consumers: tiles wv, wv + kRingCons, ...
-  for (int i = wv; i < cnt; i += kRingCons) {
-    const TileRef tr = tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, t0 + i * tstep);
-    float* lds0 = smem + (i % kRingSlots) * G::SMEM;
-    float* lds1 = lds0 + G::LDS_LEN;
-    float old_pi = 0.0f, old_pq = 0.0f;
-    if (tr.t == 0) {  // wave-uniform; scalar loads, read before this wave rewrites them
-      using cf = const __attribute__((address_space(4))) float*;
-      const int s = __builtin_amdgcn_readfirstlane(tr.s);
-      old_pi = ((cf)a.prev0)[s];
-      old_pq = ((cf)a.prev1)[s];
-    }
-    {
-      int spin = 0;
-      while (lds_peek(full + 4 * (i % kRingSlots)) != i / kRingSlots + 1) {
-        if (++spin > kRingSpin) return;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {
-      edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, lane, n, ns, [&](int e, float v0, float v1) {
-        lds0[e] = v0;
-        lds1[e] = v1;
-      });
-      wave_sync();
-    }
-    // both channels: fir_tile's scan (SGPR taps in NPASS passes)
-    const int lbase = D * R * lane;
-    float acc0[R], acc1[R];
-    if (a.ablate == 2) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        acc0[r] = lds0[lbase + r];
-        acc1[r] = lds1[lbase + r];
-      }
-    } else {
-      scan_one<D, T, R, FMA>(lds0 + lbase, acc0, h);
-      scan_one<D, T, R, FMA>(lds1 + lbase, acc1, h);
-    }
-    // the slot is read (tile 0 keeps it for the block's tail strip)
-    if (tr.t != 0) {
-      wave_sync();
-      if (lane == 0) lds_poke(freew + 4 * (i % kRingSlots), i / kRingSlots + 1);
-    }
-    float pI = __shfl_up(acc0[R - 1], 1, 64);
-    float pQ = __shfl_up(acc1[R - 1], 1, 64);
-    const bool first = tr.t == 0 && lane == 0;
-    if (first) {
-      pI = old_pi;
-      pQ = old_pq;
-    }
-    float d[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) d[r] = demod_one(acc0[r], acc1[r], r ? acc0[r - 1] : pI, r ? acc1[r - 1] : pQ);
-    const long long m0 = tr.m_start + (long long)R * lane;
-    float* o = a.out + (long long)tr.s * a.out_stride;
-    const bool vec = ((reinterpret_cast<uintptr_t>(o) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
-    if (lane >= 1 || first) {
-      if (vec && m0 + R <= nout) {
-        if constexpr (R == 2) {
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          if constexpr (SDR_OUT_NT)
-            __builtin_nontemporal_store(f2{d[0], d[1]}, reinterpret_cast<f2*>(o + m0));
-          else
-            *reinterpret_cast<f2*>(o + m0) = f2{d[0], d[1]};
-        } else {
-#pragma unroll
-          for (int r = 0; r < R; ++r) o[m0 + r] = d[r];
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-          if (m0 + r < nout) o[m0 + r] = d[r];
-      }
-    }
-    if (tr.t == 0) {
-      // state carry, as fir_tile_grp: the block's last STRIP inputs into the
-      // slot, prev_* recomputed in the reference's order, state rewritten
-      wave_sync();
-      for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
-        float v0[4], v1[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = j0 + u * NTH + lane;
-          const long long p = n - G::STRIP + j;
-          v0[u] = v1[u] = 0.0f;
-          if (j < G::STRIP) {
-            v0[u] = edge_at<SRC>(tr.x0, tr.iq, 0, tr.st0, ns, n, p);
-            v1[u] = edge_at<SRC>(tr.x1, tr.iq, 1, tr.st1, ns, n, p);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = j0 + u * NTH + lane;
-          if (j < G::STRIP) {
-            lds0[j] = v0[u];
-            lds1[j] = v1[u];
-          }
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0);
-      wave_sync();
-      if (lane < 2) {
-        using hconst = const __attribute__((address_space(4))) float*;
-        const hconst hc = (hconst)h;
-        const float* sp = (lane == 0 ? lds0 : lds1) + (G::STRIP - D);
-        float y = 0.0f;
-#pragma unroll 8
-        for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
-        (lane == 0 ? a.prev0 : a.prev1)[tr.s] = y;
-      }
-      if (ns <= G::STRIP) {
-        for (int j = lane; j < ns; j += NTH) {
-          tr.st0[j] = lds0[G::STRIP - ns + j];
-          tr.st1[j] = lds1[G::STRIP - ns + j];
-        }
-      } else {
-        for (int j = lane; j < ns; j += NTH) {
-          tr.st0[j] = in_at<SRC>(tr.x0, tr.iq, 0, n - ns + j);
-          tr.st1[j] = in_at<SRC>(tr.x1, tr.iq, 1, n - ns + j);
-        }
-      }
-      wave_sync();
-      if (lane == 0) lds_poke(freew + 4 * (i % kRingSlots), i / kRingSlots + 1);
-    }
-  }
-}
-
 // ---------------------------------------------------------- generic path --
 // Any D / T / ns the tiled kernel is not instantiated for.  One thread per
 // output sample, same operation order; x~ read straight from global memory.
@@ -1707,18 +1377,15 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   a.ablate = ablate;
   static const int persist_env = env_int("SDR_FIR_PERSIST", -1);  // A/B
   if (persist_env >= 0) persist = persist_env != 0;
-  if (TM == 2 || persist) {  // VGPR taps: persistent groups only
+  if (persist) {
     // a CU's LDS (160 KiB on gfx950, read from the device), less the claim counter
     const long long kLds = (long long)device_lds_bytes() - 64;
     constexpr long long slice = (long long)G::SMEM * sizeof(float);
     if (kLds < slice) return hipErrorInvalidConfiguration;
     static const int wpg_env = env_int("SDR_FIR_WPG", 0);  // timing experiments
-    // waves per CU: 16 (4 per SIMD at <= 128 VGPRs), TM 2: kVtWaves (3 per SIMD)
-    constexpr long long kWaveCap = TM == 2 ? kVtWaves : 16;
-    long long wpg = std::min<long long>(kWaveCap, kLds / slice);
+    long long wpg = std::min<long long>(16, kLds / slice);
     if (wpg_env > 0) wpg = std::min<long long>(wpg, wpg_env);
-    const long long wg_per_cu =
-        std::max<long long>(1, std::min<long long>(TM == 2 ? kVtWaves / wpg : 32 / wpg, kLds / (wpg * slice)));
+    const long long wg_per_cu = std::max<long long>(1, std::min<long long>(32 / wpg, kLds / (wpg * slice)));
     long long groups = std::min<long long>(ncu * wg_per_cu, (total + wpg - 1) / wpg);
     // timing experiments: about k tiles per wave, as many groups as that takes
     static const int wave_tiles = env_int("SDR_FIR_WAVE_TILES", 0);
@@ -1755,9 +1422,8 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
     blocks = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
   }
   const size_t lds = (size_t)G::SMEM * sizeof(float);
-  if constexpr (TM == 1)
-    hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds,
-                       st, a, h);
+  hipLaunchKernelGGL((fir_tile<D, T, R, NW, NCH, DEMOD, SRC, TM, FMA>), dim3((unsigned)blocks), dim3(G::NTH), lds, st,
+                     a, h);
   return hipGetLastError();
 }
 
@@ -1778,43 +1444,6 @@ hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
   return hipGetLastError();
 }
 
-// fir_ring launch: one persistent workgroup per CU, a contiguous run of
-// tiles each
-template <int D, int T, int R, bool FMA = false>
-hipError_t run_ring(const FirLaunch& a0, const float* h, hipStream_t st) {
-  using G = Geom<D, T, R, true, 1>;
-  FirLaunch a = a0;
-  const long long nout = a.n / D;
-  a.tiles_per_stream = nout > G::E ? (int)((nout - G::E + G::ADV - 1) / G::ADV) : 1;
-  const long long total = (long long)a.tiles_per_stream * a.nstreams;
-  if (total <= 0 || total > 0x7fffffffLL) return hipErrorInvalidValue;
-  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
-  a.ablate = ablate;
-  const long long ncu = device_cu_count();
-  long long grid = std::min<long long>(ncu, total);
-  static const int walk_env = env_int("SDR_RING_WALK", 1);  // A/B
-  if (walk_env && grid >= 8 && total >= 64) {
-    grid -= grid % 8;
-    a.walk = 1;
-    a.slab = (int)((total + 7) / 8);
-  } else {
-    a.walk = 0;
-    a.tiles_per_wg = (int)((total + grid - 1) / grid);
-    grid = (total + a.tiles_per_wg - 1) / a.tiles_per_wg;
-  }
-  const size_t lds = (size_t)kRingSlots * G::SMEM * sizeof(float) + 2 * kRingSlots * sizeof(int);
-  if ((long long)lds > (long long)device_lds_bytes()) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((fir_ring<D, T, R, FMA>), dim3((unsigned)grid), dim3(64 * (kRingCons + kRingLoad)), lds, st, a, h);
-  return hipGetLastError();
-}
-
-// the f32 fused front end (D = 10) on fir_ring (SDR_FIR_RING=1; read per
-// launch, so a test runs both)
-bool ring_enabled() {
-  const char* e = std::getenv("SDR_FIR_RING");
-  return e && std::atoi(e) != 0;
-}
-
 // The fused f32 front end runs fir_tile_sc (same box: 0.0978-0.0990 vs
 // 0.1015-0.1056 ms on cfg2, profiles/r03_ab/cfg2_split_channel.txt);
 // SDR_FIR_SC=0 selects fir_tile (read per launch, so a test runs both)
@@ -1828,15 +1457,6 @@ bool sc_enabled() {
 bool sc_u8_enabled() {
   const char* e = std::getenv("SDR_FIR_SC_U8");
   return !e || std::atoi(e) != 0;
-}
-
-// the u8 wire path (D = 10) on fir_tile_grp with VGPR taps (TM 2), opt-in
-// (SDR_FIR_VT_U8=1): 0.0845 vs 0.0814 ms on cfg2u8, scan-only 72.5 vs 73.9 us
-// (profiles/r04f/) -- the taps' location does not bound the scan (read per
-// launch, so a test runs both)
-bool vt_u8_enabled() {
-  const char* e = std::getenv("SDR_FIR_VT_U8");
-  return e && std::atoi(e) != 0;
 }
 
 // Tile shape per decimation factor: R outputs per lane, one wave per
@@ -1880,15 +1500,6 @@ hipError_t dispatch_tile(const FirLaunch& a, const float* h, hipStream_t st, boo
         // fir_tile_sc by default (SDR_FIR_SC=0 / SDR_FIR_SC_U8=0: fir_tile,
         // the u8 wire format on persistent groups) -- DESIGN.md 4.1, 5.2
         case 10:
-          // u8 wire format: persistent groups with VGPR taps (SDR_FIR_VT_U8=0:
-          // the split-channel kernel)
-          if constexpr (SRC == Src::U8)
-            if (vt_u8_enabled())
-              return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 2, true>(a, h, st, true, 64)
-                           : run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 2>(a, h, st, true, 64);
-          if constexpr (SRC == Src::F32)
-            if (ring_enabled())
-              return a.fma ? run_ring<10, 101, 2, true>(a, h, st) : run_ring<10, 101, 2>(a, h, st);
           if (SRC == Src::F32 ? sc_enabled() : sc_u8_enabled())
             return a.fma ? run_tile_sc<10, 101, 2, SRC, true>(a, h, st) : run_tile_sc<10, 101, 2, SRC>(a, h, st);
           return a.fma ? run_tile<10, 101, 2, 1, NCH, DEMOD, SRC, 1, true>(a, h, st, kPersistFused, 64)

@@ -60,12 +60,10 @@ def _planar_batch(sdrhip, ctx, nstreams, n, seed, stride=None):
     return d_I, d_Q
 
 
-@pytest.mark.parametrize("kernel", ["tile", "sc", "ring"])
+@pytest.mark.parametrize("kernel", ["tile", "sc"])
 def test_cfg2_full_f32_two_steps(gpu_ctx, oracle, built_lib, monkeypatch, kernel):
-    """kernel: fir_tile, fir_tile_sc (SDR_FIR_SC=1) or fir_ring (SDR_FIR_RING=1);
-    the bench's launches either way."""
+    """kernel: fir_tile, or fir_tile_sc (SDR_FIR_SC=1); the bench's launches either way."""
     monkeypatch.setenv("SDR_FIR_SC", "0" if kernel == "tile" else "1")
-    monkeypatch.setenv("SDR_FIR_RING", "1" if kernel == "ring" else "0")
     sdrhip = built_lib
     S, n, D = 1024, 65540, 10
     nout = n // D

@@ -23,13 +23,11 @@ def _blocks(a, block, nblk):
 
 # ------------------------------------------------------------ golden, host API
 
-@pytest.mark.parametrize("kernel", ["tile", "sc", "ring"])
+@pytest.mark.parametrize("kernel", ["tile", "sc"])
 @pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
 def test_frontend_fused_golden(gpu_ctx, oracle, manifest, monkeypatch, name, kernel):
-    """kernel: the fused f32 front end on fir_tile, on fir_tile_sc (SDR_FIR_SC=1),
-    or on the loader-ring fir_ring (SDR_FIR_RING=1)."""
+    """kernel: the fused f32 front end on fir_tile, or on fir_tile_sc (SDR_FIR_SC=1)."""
     monkeypatch.setenv("SDR_FIR_SC", "0" if kernel == "tile" else "1")
-    monkeypatch.setenv("SDR_FIR_RING", "1" if kernel == "ring" else "0")
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     I, Q = oracle.u8_to_planar(g["iq_u8"])
@@ -40,13 +38,11 @@ def test_frontend_fused_golden(gpu_ctx, oracle, manifest, monkeypatch, name, ker
         assert_bits(np.concatenate([si, sq, prev]), g["states"][b], f"{name} states[{b}]")
 
 
-@pytest.mark.parametrize("kernel", ["grp", "sc", "vt"])
+@pytest.mark.parametrize("kernel", ["grp", "sc"])
 @pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
 def test_frontend_u8_golden(gpu_ctx, manifest, monkeypatch, name, kernel):
-    """u8 wire front end on each kernel: fir_tile_grp with SGPR taps (grp),
-    fir_tile_sc (sc), fir_tile_grp with VGPR taps (vt, SDR_FIR_VT_U8=1)."""
+    """u8 wire front end on each kernel: fir_tile_grp (grp) and fir_tile_sc (sc)."""
     monkeypatch.setenv("SDR_FIR_SC_U8", "0" if kernel == "grp" else "1")
-    monkeypatch.setenv("SDR_FIR_VT_U8", "1" if kernel == "vt" else "0")
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     si, sq, prev = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
@@ -125,7 +121,7 @@ def test_fir_decim_vs_oracle(gpu_ctx, oracle, D, ntaps, ns, n):
 @pytest.mark.parametrize("D,n,ns", [(10, 5130, 100), (10, 5130, 150), (10, 2000, 200), (5, 4105, 100),
                                     (5, 4105, 128), (10, 110, 100), (10, 200, 180), (10, 130, 120),
                                     (10, 65530, 100), (10, 65550, 300)])
-@pytest.mark.parametrize("kernel", ["tile", "sc", "vt", "ring"])
+@pytest.mark.parametrize("kernel", ["tile", "sc"])
 def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, monkeypatch, D, n, ns, kernel):
     """Fused front end (f32 and u8 wire) where the tiled kernel's edge
     handling matters: n % 4 != 0 (a chunk straddles the block end), state
@@ -135,8 +131,6 @@ def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, monkeypatch, D, n, ns, k
 
     monkeypatch.setenv("SDR_FIR_SC", "0" if kernel == "tile" else "1")
     monkeypatch.setenv("SDR_FIR_SC_U8", "0" if kernel == "tile" else "1")
-    monkeypatch.setenv("SDR_FIR_VT_U8", "1" if kernel == "vt" else "0")
-    monkeypatch.setenv("SDR_FIR_RING", "1" if kernel == "ring" else "0")
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = fm_iq_u8(n * 3, seed=D * 100 + n + ns)
     st = {k: [np.zeros(ns, np.float32), np.zeros(ns, np.float32), np.zeros(2, np.float32)]
@@ -324,7 +318,7 @@ def _fm_streams(nstreams, n, seed=5):
     return np.stack([fm_iq_u8(n, seed=seed + s) for s in range(nstreams)])
 
 
-@pytest.mark.parametrize("src", ["f32", "f32sc", "f32ring", "u8", "u8sc", "u8vt"])
+@pytest.mark.parametrize("src", ["f32", "f32sc", "u8", "u8sc"])
 @pytest.mark.parametrize("D,n", [(10, 65540), (10, 5120), (5, 40960)])
 def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, src, D, n):
     """nstreams independent streams x 3 consecutive blocks through the
@@ -333,9 +327,7 @@ def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, src
     sdrhip = built_lib
     monkeypatch.setenv("SDR_FIR_SC", "1" if src == "f32sc" else "0")
     monkeypatch.setenv("SDR_FIR_SC_U8", "1" if src == "u8sc" else "0")
-    monkeypatch.setenv("SDR_FIR_VT_U8", "1" if src == "u8vt" else "0")
-    monkeypatch.setenv("SDR_FIR_RING", "1" if src == "f32ring" else "0")
-    src = src[:-4] if src.endswith("ring") else (src[:-2] if src.endswith(("sc", "vt")) else src)
+    src = src[:-2] if src.endswith("sc") else src
     nstreams, nblk = 6, 3
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = _fm_streams(nstreams, n * nblk)
