@@ -335,7 +335,7 @@ struct MfArgs {
   long long n, x_stride;  // halves
   const float* h;
   int ntaps, kd, lc;      // taps, K extent (multiple of 16), halves per tap copy
-  const _Float16* state;
+  _Float16* state;        // read by each stream's first workgroup, then rewritten by it
   int ns;
   float* y;
   long long y_stride;
@@ -358,13 +358,44 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   const long long pb = m0 - a.ntaps;                   // stream position of image element 0 (multiple of 8)
   const _Float16* xs = a.x + (long long)s * a.x_stride;
   const _Float16* st = a.state + (long long)s * a.ns;
-  // ---- stage the input image: 16-B chunks, element-wise at the block edges
-  for (int c = tid; c < (a.span >> 3); c += 64 * kMfWaves) {
-    const long long p = pb + 8LL * c;
-    _Float16* d = img + mf_pad(8 * c);
-    if (p >= 0 && p + 8 <= a.n) {
-      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(xs + p);
-    } else {
+  // ---- issue every load first (image chunks, taps), then write LDS: a
+  // load-then-store loop waits out one memory latency per iteration.
+  // kMfChunks covers the image at T <= 4096 (span <= 12,288 halves) and
+  // kMfTaps the reversed taps (a.lc + 40 <= 4,264 halves).
+  constexpr int kNT = 64 * kMfWaves, kMfChunks = 6, kMfTaps = 17;
+  const int nchunk = a.span >> 3;
+  // every register defined (clamped, in-bounds addresses: n >= 8 on this
+  // path), so the array stays in VGPRs; the edge chunks are rewritten below
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct defeats SROA here)
+  u32x4 iv[kMfChunks];
+#pragma unroll
+  for (int k = 0; k < kMfChunks; ++k) {
+    long long p = pb + 8LL * (tid + k * kNT);
+    p = p < 0 ? 0 : (p > a.n - 8 ? a.n - 8 : p);
+    iv[k] = *reinterpret_cast<const u32x4*>(xs + (p & ~7LL));
+  }
+  // the reversed f16 taps once, hb[j] = hr[j - 32], hr[v] = h[T-1-v]
+  // (coalesced f32 loads); the tap copies are built from them in LDS below
+  _Float16* hb = hcp + 8 * a.lc;
+  const int nhb = a.lc + 40;
+  float hv[kMfTaps];
+#pragma unroll
+  for (int k = 0; k < kMfTaps; ++k) {
+    const int v = tid + k * kNT - 32;
+    hv[k] = (v >= 0 && v < a.ntaps) ? a.h[a.ntaps - 1 - v] : 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < kMfChunks; ++k) {
+    const int c = tid + k * kNT;
+    if (c < nchunk) *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
+  }
+  // block edges (the stream's first and last workgroups), element-wise over
+  // the clamped chunks: the carried state before 0, zeros past n
+  if (pb < 0 || pb + a.span > a.n) {
+    for (int c = tid; c < nchunk; c += kNT) {
+      const long long p = pb + 8LL * c;
+      if (p >= 0 && p + 8 <= a.n) continue;
+      _Float16* d = img + mf_pad(8 * c);
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const long long q = p + r;
@@ -372,11 +403,22 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
       }
     }
   }
-  // ---- the tap copies: copy q, element w = hr[w + q - 32], hr[v] = h[T-1-v]
-  for (int e = tid; e < 8 * a.lc; e += 64 * kMfWaves) {
-    const int q = e / a.lc, w = e - q * a.lc;
-    const int v = w + q - 32;
-    hcp[e] = (v >= 0 && v < a.ntaps) ? (_Float16)a.h[a.ntaps - 1 - v] : (_Float16)0;
+#pragma unroll
+  for (int k = 0; k < kMfTaps; ++k)
+    if (tid + k * kNT < nhb) hb[tid + k * kNT] = (_Float16)hv[k];
+  __syncthreads();
+  // the stream's first workgroup is the only reader of the old state (staged
+  // above): it writes the new one, the block's last ns inputs
+  // (src/filter.cpp:82), after that barrier
+  if (m0 == 0)
+    for (int i = tid; i < a.ns; i += 64 * kMfWaves) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
+  const int cpr = a.lc >> 3;  // 16-B chunks per copy
+  for (int c = tid; c < 8 * cpr; c += 64 * kMfWaves) {
+    const int q = c / cpr, w0 = 8 * (c - q * cpr);
+    half8 v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = hb[w0 + q + k];
+    *reinterpret_cast<half8*>(hcp + q * a.lc + w0) = v;
   }
   __syncthreads();
   const int i = lane & 31, hh = lane >> 5;
@@ -466,7 +508,12 @@ __global__ __launch_bounds__(kWG) void f32_to_f16(const float* __restrict__ x, l
 
 }  // namespace
 
-bool fir_f16_uses_mfma(int ntaps) { return ntaps % 8 == 0 && env_int("SDR_F16_MFMA", kF16MfmaDefault) != 0; }
+// T <= 4096: the image, tap copies and reversed taps fit the LDS (about
+// 106 KiB at 4096), and no workgroup but a stream's first reaches into the
+// state (T < kMfOut), which lets that one commit the new state in-kernel
+bool fir_f16_uses_mfma(int ntaps) {
+  return ntaps % 8 == 0 && ntaps <= 4096 && env_int("SDR_F16_MFMA", kF16MfmaDefault) != 0;
+}
 
 size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32); }
 
@@ -476,7 +523,7 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
   // the MFMA form: T % 8 == 0 keeps the staged image's 16-B chunks aligned
   // (x rows are 16-B aligned, checked by the caller); SDR_F16_MFMA=0 selects
   // the dot2 kernel below (A/B, tests)
-  if (fir_f16_uses_mfma(ntaps)) {
+  if (fir_f16_uses_mfma(ntaps) && n >= 8) {  // (n >= 8: the clamped staging loads stay in the row)
     MfArgs a;
     a.x = static_cast<const _Float16*>(x);
     a.n = n;
@@ -485,20 +532,18 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.ntaps = ntaps;
     a.kd = (ntaps + 31 + 95) / 96 * 96;  // an even number of 3-step groups (zero taps past the band)
     a.lc = (a.kd + 40 + 7) / 8 * 8;
-    a.state = static_cast<const _Float16*>(state);
+    a.state = static_cast<_Float16*>(state);
     a.ns = ns;
     a.y = y;
     a.y_stride = y_stride;
     a.wg_per_stream = (int)((n + kMfOut - 1) / kMfOut);
     a.span = kMfOut + a.kd - 32;
-    const size_t lds = ((size_t)mf_pad(a.span) + 8 + 8 * (size_t)a.lc) * sizeof(_Float16);
+    // image, 8 tap copies, the reversed taps (a.lc + 40 halves)
+    const size_t lds = ((size_t)mf_pad(a.span) + 8 + 9 * (size_t)a.lc + 40) * sizeof(_Float16);
     const long long blocks = (long long)a.wg_per_stream * nstreams;
-    if (blocks > 0x7fffffffLL || lds > 160 * 1024) return hipErrorInvalidValue;
+    if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
+    // one launch: each stream's first workgroup commits the state itself
     hipLaunchKernelGGL(fir_long_mfma, dim3((unsigned)blocks), dim3(64 * kMfWaves), lds, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || ns <= 0) return e;
-    hipLaunchKernelGGL(long_commit_h, dim3((ns + kWG - 1) / kWG, (unsigned)nstreams), dim3(kWG), 0, st,
-                       static_cast<const _Float16*>(x), n, x_stride, static_cast<_Float16*>(state), ns);
     return hipGetLastError();
   }
   const int len = (int)fir_long_h_pairs(ntaps);

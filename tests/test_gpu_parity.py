@@ -271,7 +271,8 @@ def test_resample_many_streams(gpu_ctx, oracle, built_lib, up, down, cnt, nstrea
 
 
 @pytest.mark.parametrize("kernel", ["mfma", "dot2"])
-@pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000), (256, 8200), (8, 704)])
+@pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000), (256, 8200), (8, 704),
+                                    (4096, 20000)])
 def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, monkeypatch, ntaps, n, kernel):
     """BASELINE config 5's fp16 arm (fp16 storage, fp32 accumulation -- the
     Toeplitz-GEMM v_mfma_f32_32x32x16_f16 kernel for T % 8 == 0, else / under
