@@ -220,11 +220,12 @@ int sdr_resample_plan_destroy(sdr_ctx *ctx, sdr_resample_plan *plan);
 /* BASELINE config 5's fp16 arm of blockConvolveFIR (src/filter.cpp:66-83):
  * x and state are fp16 (IEEE binary16, [nstreams][x_stride] / [nstreams][ns]),
  * taps fp32 (rounded to fp16 inside), y fp32.  fp32 accumulation of fp16
- * products (v_dot2_f32_f16).  NOT bit-exact with the reference -- a
- * tolerance arm; the fp32 calls above are the exact path.  Rows must be
- * 16-B aligned. */
+ * products: a Toeplitz GEMM on v_mfma_f32_32x32x16_f16 when ntaps % 8 == 0,
+ * ntaps <= 4096 and n >= 8 (one launch), else v_dot2_f32_f16.  NOT bit-exact
+ * with the reference -- a tolerance arm; the fp32 calls above are the exact
+ * path.  Rows must be 16-B aligned. */
 /* Which kernel sdr_fir_block_f16_dev runs for ntaps under the current
- * environment: 1 = the Toeplitz GEMM on v_mfma_f32_32x32x16_f16, 0 = v_dot2. */
+ * environment (blocks of n >= 8): 1 = the MFMA Toeplitz GEMM, 0 = v_dot2. */
 int sdr_fir_block_f16_kernel(int ntaps);
 int sdr_fir_block_f16_dev(sdr_ctx *ctx, const void *x, long long n, int nstreams, long long x_stride,
                           const float *h, int ntaps, void *state, int ns, float *y, long long y_stride);
