@@ -95,14 +95,31 @@ SDR_HD inline unsigned lo_bits(double d) { return (unsigned)__builtin_bit_cast(u
 SDR_HD inline unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
 SDR_HD inline unsigned mid_score(double d) { return (lo_bits(d) << 3) + kMidBias; }
 
+// The oscillator's argument over the next chunk's 8 steps stays inside the
+// reduction's exhaustively checked range, |trigArg| < 2^26:
+//   trigArg = step * trigOffset' + phaseEst',  trigOffset' <= trigOffset + 8,
+//   |phaseEst'| <= |phaseEst| + 8 |integrator| + 138  (|Kp|, |Ki| <= 1, |errorD| <= pi),
+// bounded here in fp32 with stepf >= |step| (step_bound) and margins well
+// above the few roundings of the bound itself.  trigOffset may sit AT 2^24:
+// there the reference's `trigOffset++` stops advancing (fp32), which the
+// fast step computes the same way -- a receiver reaches it after 2^24
+// samples (70 s at 240 kHz) and stays there.
+SDR_HD inline bool arg_ok(float integrator, float phaseEst, float trigOffset, float stepf) {
+  const float ph = __builtin_fmaf(__builtin_fabsf(integrator), 16.0f, __builtin_fabsf(phaseEst) + 256.0f);
+  return __builtin_fmaf(stepf, trigOffset + 8.0f, ph) < 0x1p26f;
+}
+// |step| rounded up to fp32 with a relative margin (once per launch)
+SDR_HD inline float step_bound(double step) { return (float)(__builtin_fabs(step) * (1.0 + 0x1p-20)); }
+
 // Chunk guard: the state at a chunk's start keeps every step of the next 8
 // inside the certified domain (|Kp|, |Ki| <= 1 is the caller's launch-time
 // condition).  Written with & so it is straight-line code.
-SDR_HD inline bool chunk_ok(float fbI, float fbQ, float integrator, float phaseEst, float trigOffset) {
+SDR_HD inline bool chunk_ok(float fbI, float fbQ, float integrator, float phaseEst, float trigOffset, float stepf) {
   const float aI = __builtin_fabsf(fbI), aQ = __builtin_fabsf(fbQ);
-  return (int)(trigOffset >= 0.0f) & (int)(trigOffset < 0x1p24f) & (int)(__builtin_fabsf(phaseEst) < 0x1p24f) &
-         (int)(__builtin_fabsf(integrator) < 0x1p20f) & (int)(aI <= 1.0f) & (int)(aQ <= 1.0f) &
-         ((int)(aI >= 0x1p-60f) | (int)(fbI == 0.0f)) & ((int)(aQ >= 0x1p-60f) | (int)(fbQ == 0.0f));
+  return (int)(trigOffset >= 0.0f) & (int)(trigOffset <= 0x1p24f) & (int)(__builtin_fabsf(phaseEst) < 0x1p24f) &
+         (int)(__builtin_fabsf(integrator) < 0x1p20f) & (int)arg_ok(integrator, phaseEst, trigOffset, stepf) &
+         (int)(aI <= 1.0f) & (int)(aQ <= 1.0f) & ((int)(aI >= 0x1p-60f) | (int)(fbI == 0.0f)) &
+         ((int)(aQ >= 0x1p-60f) | (int)(fbQ == 0.0f));
 }
 
 // Chunk guard on the inputs: every sample v of a certified chunk is 0 or
@@ -277,11 +294,12 @@ SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned&
 
 // The closing check of a chunk that ran the fast path from a chunk_ok state:
 // phaseEst, integrator and trigOffset finite and small enough for the next
-// chunk (trigOffset only grows; the feedback floats are sin / cos results of
-// arguments in the domain, so 0 or >= 2^-54 -- see chunk_ok).  A NaN
-// anywhere in the chunk reaches phaseEst, and fails here.
-SDR_HD inline bool chunk_end_ok(float integrator, float phaseEst, float trigOffset) {
-  return __builtin_fmaf(__builtin_fabsf(integrator), 16.0f, __builtin_fabsf(phaseEst)) + trigOffset < 0x1p24f;
+// chunk (trigOffset only grows, up to 2^24; the feedback floats are sin /
+// cos results of arguments in the domain, so 0 or >= 2^-54 -- see
+// chunk_ok).  A NaN anywhere in the chunk reaches phaseEst, and fails here.
+SDR_HD inline bool chunk_end_ok(float integrator, float phaseEst, float trigOffset, float stepf) {
+  return (int)(__builtin_fmaf(__builtin_fabsf(integrator), 16.0f, __builtin_fabsf(phaseEst)) < 0x1p24f) &
+         (int)(trigOffset <= 0x1p24f) & (int)arg_ok(integrator, phaseEst, trigOffset, stepf);
 }
 
 }  // namespace pllfast

@@ -107,8 +107,9 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   using rot_t = std::true_type;
   using poly_t = std::false_type;
   const bool gains_ok = __builtin_fabsf(Kp) <= 1.0f && __builtin_fabsf(Ki) <= 1.0f;  // chunk_ok's premise
+  const float stepf = pllfast::step_bound(step);
   // chunk_ok of the state a chunk starts from (the previous chunk's closing check)
-  bool start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
+  bool start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset, stepf);
   // The chain is latency-bound (one lane per stream).  Inputs are loaded one
   // chunk ahead into registers, so no step waits on memory: a per-sample
   // load put a full load latency -- and the previous step's store, which
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
         fast_step(buf[j], rot_t{});
         ar[k0 + j + 1] = arg;
       }
-      start_ok = pllfast::chunk_end_ok(integrator, phaseEst, trigOffset);
+      start_ok = pllfast::chunk_end_ok(integrator, phaseEst, trigOffset, stepf);
       // 2: timing experiment only (no re-run)
       if (FAST == 2 || !__any(score < pllfast::kCertified || !start_ok)) return;
       fbI = s0;
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
       if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
     }
     if constexpr (FAST) {
-      start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset);
+      start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset, stepf);
       // the next chunk's first step rotates from the oscillator of this
       // chunk's last argument (the library's floats are within an ulp of it)
       float tq, ti;

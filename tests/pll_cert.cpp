@@ -129,7 +129,8 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
   Pll r, f;
   r.trig = f.trig = trig0;
   long long bad_args = 0;
-  bool start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig);
+  const float stepf = step_bound(step);
+  bool start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig, stepf);
   Osc osc{};  // the kernel's: every step but the first rotates back from the previous step's oscillator
   auto lib_step = [&](Pll& p, float v) {
     const float eI = (v == 0.0f ? 1.0f : v) * p.fbI;
@@ -163,13 +164,13 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
       fa[j] = (float)(step * (double)f.trig + (double)f.phase);
       sincos_fast<HostOps>(fa[j], f.fbQ, f.fbI, score, osc);
     }
-    start_ok = chunk_end_ok(f.integ, f.phase, f.trig);
+    start_ok = chunk_end_ok(f.integ, f.phase, f.trig, stepf);
     const bool bad = score < kCertified || !start_ok;
     if (bad) {
       ++*reruns;
       f = saved;
       for (long long j = 0; j < m; ++j) fa[j] = lib_step(f, in[k0 + j]);
-      start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig);
+      start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig, stepf);
       float tq, ti;
       unsigned unused = 0u;
       sincos_fast<HostOps>(fa[m - 1], tq, ti, unused, osc);  // the kernel's refresh after a re-run
@@ -243,7 +244,8 @@ int main(int argc, char** argv) {
     for (long long k = 0; k < L; ++k)
       pil[k] = (float)(amp * std::cos(2 * M_PI * f / 240e3 * (double)k + ph) + G(g));
     for (long long k = 0; k < L; k += 997) pil[k] = 0.0f;
-    const float trig0 = s % 3 == 0 ? 0.0f : (s % 3 == 1 ? 3.0e6f : 1.6e7f);
+    // 16,770,000: trigOffset reaches 2^24 (where fp32 ++ stops) mid-run
+    const float trig0 = s % 4 == 0 ? 0.0f : (s % 4 == 1 ? 3.0e6f : (s % 4 == 2 ? 1.6e7f : 16770000.0f));
     pll_bad += pll_compare(pil, L, trig0, &reruns);
     steps += L;
   }

@@ -573,14 +573,15 @@ def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix, n):
             assert_bits(dev_st[s], ost[s], f"pll state stream {s} block {b}")
 
 
-@pytest.mark.parametrize("trig0", [0.0, 3.0e6, 1.6e7])
+@pytest.mark.parametrize("trig0", [0.0, 3.0e6, 1.6e7, 16773000.0, 16777216.0])
 def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
     """The PLL kernel's certified short-chain path (csrc/pll_fast.hpp, the
     default) against its library-routine path (SDR_PLL_FAST=0) on 512 streams
     x 8,192 samples, bitwise, and 8 streams of it against the oracle.  trig0
     starts the oscillator's trigOffset late (oscillator arguments up to ~8e6
-    rad: the reduction's large-argument range; 1.6e7 reaches fp32's integer
-    limit, where trigOffset++ stops advancing, src/filter.cpp:212)."""
+    rad: the reduction's large-argument range); 16,773,000 crosses fp32's
+    integer limit 2^24 mid-block and 2^24 starts there -- trigOffset++ stops
+    advancing (src/filter.cpp:212), and the certified path keeps running."""
     sdrhip = built_lib
     rng = np.random.default_rng(int(trig0) + 5)
     S, n, Fs = 512, 8192, 240e3
