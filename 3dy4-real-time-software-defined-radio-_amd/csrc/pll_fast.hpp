@@ -100,7 +100,10 @@ SDR_HD inline unsigned mid_score(double d) { return (lo_bits(d) << 3) + kMidBias
 //   trigArg = step * trigOffset' + phaseEst',  trigOffset' <= trigOffset + 8,
 //   |phaseEst'| <= |phaseEst| + 8 |integrator| + 138  (|Kp|, |Ki| <= 1, |errorD| <= pi),
 // bounded here in fp32 with stepf >= |step| (step_bound) and margins well
-// above the few roundings of the bound itself.  trigOffset may sit AT 2^24:
+// above the few roundings of the bound itself (a NaN or Inf anywhere fails
+// it).  This bound is all |phaseEst| needs: past 2^24 samples the loop's
+// phase keeps growing in phaseEst, and the fast step follows it up to
+// |trigArg| < 2^26.  trigOffset may sit AT 2^24:
 // there the reference's `trigOffset++` stops advancing (fp32), which the
 // fast step computes the same way -- a receiver reaches it after 2^24
 // samples (70 s at 240 kHz) and stays there.
@@ -116,7 +119,7 @@ SDR_HD inline float step_bound(double step) { return (float)(__builtin_fabs(step
 // condition).  Written with & so it is straight-line code.
 SDR_HD inline bool chunk_ok(float fbI, float fbQ, float integrator, float phaseEst, float trigOffset, float stepf) {
   const float aI = __builtin_fabsf(fbI), aQ = __builtin_fabsf(fbQ);
-  return (int)(trigOffset >= 0.0f) & (int)(trigOffset <= 0x1p24f) & (int)(__builtin_fabsf(phaseEst) < 0x1p24f) &
+  return (int)(trigOffset >= 0.0f) & (int)(trigOffset <= 0x1p24f) &
          (int)(__builtin_fabsf(integrator) < 0x1p20f) & (int)arg_ok(integrator, phaseEst, trigOffset, stepf) &
          (int)(aI <= 1.0f) & (int)(aQ <= 1.0f) & ((int)(aI >= 0x1p-60f) | (int)(fbI == 0.0f)) &
          ((int)(aQ >= 0x1p-60f) | (int)(fbQ == 0.0f));
@@ -298,8 +301,8 @@ SDR_HD inline float atan2_rot(float y, float x, float v, const Osc& o, unsigned&
 // cos results of arguments in the domain, so 0 or >= 2^-54 -- see
 // chunk_ok).  A NaN anywhere in the chunk reaches phaseEst, and fails here.
 SDR_HD inline bool chunk_end_ok(float integrator, float phaseEst, float trigOffset, float stepf) {
-  return (int)(__builtin_fmaf(__builtin_fabsf(integrator), 16.0f, __builtin_fabsf(phaseEst)) < 0x1p24f) &
-         (int)(trigOffset <= 0x1p24f) & (int)arg_ok(integrator, phaseEst, trigOffset, stepf);
+  return (int)(__builtin_fabsf(integrator) < 0x1p20f) & (int)(trigOffset <= 0x1p24f) &
+         (int)arg_ok(integrator, phaseEst, trigOffset, stepf);
 }
 
 }  // namespace pllfast

@@ -123,11 +123,12 @@ struct Pll {
   float fbI = 1, fbQ = 0, integ = 0, phase = 0, trig = 0;
 };
 
-static long long pll_compare(const float* in, long long n, float trig0, long long* reruns) {
+static long long pll_compare(const float* in, long long n, float trig0, long long* reruns, float phase0 = 0.0f) {
   const float Kp = 0.01f * 2.666f, Ki = 0.01f * 0.01f * 3.555f;
   const double step = 2.0 * 3.14159265358979323846 * (double)(19e3f / 240e3f);
   Pll r, f;
   r.trig = f.trig = trig0;
+  r.phase = f.phase = phase0;
   long long bad_args = 0;
   const float stepf = step_bound(step);
   bool start_ok = chunk_ok(f.fbI, f.fbQ, f.integ, f.phase, f.trig, stepf);
@@ -246,7 +247,9 @@ int main(int argc, char** argv) {
     for (long long k = 0; k < L; k += 997) pil[k] = 0.0f;
     // 16,770,000: trigOffset reaches 2^24 (where fp32 ++ stops) mid-run
     const float trig0 = s % 4 == 0 ? 0.0f : (s % 4 == 1 ? 3.0e6f : (s % 4 == 2 ? 1.6e7f : 16770000.0f));
-    pll_bad += pll_compare(pil, L, trig0, &reruns);
+    // s = 23: a saturated trigOffset with phaseEst past 2^24 (the loop's
+    // phase keeps growing there, src/filter.cpp:210)
+    pll_bad += pll_compare(pil, L, s == 23 ? 16777216.0f : trig0, &reruns, s == 23 ? 2.5e7f : 0.0f);
     steps += L;
   }
   // tiny, subnormal and non-finite pilot samples (input_ok's excluded range,

@@ -573,15 +573,18 @@ def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix, n):
             assert_bits(dev_st[s], ost[s], f"pll state stream {s} block {b}")
 
 
-@pytest.mark.parametrize("trig0", [0.0, 3.0e6, 1.6e7, 16773000.0, 16777216.0])
-def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
+@pytest.mark.parametrize("trig0,phase0", [(0.0, 0.0), (3.0e6, 0.0), (1.6e7, 0.0), (16773000.0, 0.0),
+                                          (16777216.0, 0.0), (16777216.0, 2.5e7)])
+def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, phase0, monkeypatch):
     """The PLL kernel's certified short-chain path (csrc/pll_fast.hpp, the
     default) against its library-routine path (SDR_PLL_FAST=0) on 512 streams
     x 8,192 samples, bitwise, and 8 streams of it against the oracle.  trig0
     starts the oscillator's trigOffset late (oscillator arguments up to ~8e6
     rad: the reduction's large-argument range); 16,773,000 crosses fp32's
     integer limit 2^24 mid-block and 2^24 starts there -- trigOffset++ stops
-    advancing (src/filter.cpp:212), and the certified path keeps running."""
+    advancing (src/filter.cpp:212), and the certified path keeps running;
+    phase0 = 2.5e7 starts phaseEst past 2^24 as well (the loop's phase keeps
+    growing there)."""
     sdrhip = built_lib
     rng = np.random.default_rng(int(trig0) + 5)
     S, n, Fs = 512, 8192, 240e3
@@ -590,7 +593,7 @@ def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, monkeypatch):
     x = (rng.uniform(0.01, 0.3, S)[:, None] * np.cos(2 * np.pi * f / Fs * t + rng.uniform(0, 6.3, S)[:, None])
          + rng.normal(0, 0.01, (S, n))).astype(np.float32)
     x[:, ::1013] = 0.0
-    st0 = np.tile(np.array([1, 0, 0, 0, trig0, 1], np.float32), S)
+    st0 = np.tile(np.array([1, 0, 0, phase0, trig0, 1], np.float32), S)
     A = sdrhip.DeviceArray
     d_x = A.from_numpy(gpu_ctx, x)
     res = {}
