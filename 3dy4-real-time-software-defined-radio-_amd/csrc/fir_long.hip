@@ -341,6 +341,7 @@ struct MfArgs {
   long long y_stride;
   int wg_per_stream;
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
+  int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA
 };
 
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
@@ -372,6 +373,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   for (int k = 0; k < kMfChunks; ++k) {
     long long p = pb + 8LL * (tid + k * kNT);
     p = p < 0 ? 0 : (p > a.n - 8 ? a.n - 8 : p);
+    if (a.ablate == 1) p = 0;  // (ablation 1: one cached chunk instead of the stream)
     iv[k] = *reinterpret_cast<const u32x4*>(xs + (p & ~7LL));
   }
   // the reversed f16 taps once, hb[j] = hr[j - 32], hr[v] = h[T-1-v]
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // G steps per group; the next group's 3 G fragments are read while this
   // group's 2 G MFMAs run (kd is a multiple of 32 G: an even group count)
   constexpr int G = 3;
-  const int ngrp = a.kd / (16 * G);
+  const int ngrp = a.ablate == 2 ? 0 : a.kd / (16 * G);  // (ablation 2: no MFMA)
   half8 av[G], bv[G][kMfNT];
   auto fetch = [&](int g0, half8 (&aa)[G], half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -538,6 +540,8 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.y_stride = y_stride;
     a.wg_per_stream = (int)((n + kMfOut - 1) / kMfOut);
     a.span = kMfOut + a.kd - 32;
+    static const int ablate = env_int("SDR_ABLATE", 0);
+    a.ablate = ablate;
     // image, 8 tap copies, the reversed taps (a.lc + 40 halves)
     const size_t lds = ((size_t)mf_pad(a.span) + 8 + 9 * (size_t)a.lc + 40) * sizeof(_Float16);
     const long long blocks = (long long)a.wg_per_stream * nstreams;
