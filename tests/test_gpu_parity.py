@@ -311,6 +311,40 @@ def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, monkeypatch, ntaps,
                               x[:, -ns:].astype(np.float16)), "fp16 state"
 
 
+@pytest.mark.parametrize("kernel", ["mfma", "dot2"])
+def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, monkeypatch, kernel):
+    """The fp16 arm on padded rows (x_stride, y_stride > n) over 3 streams, two
+    blocks: each stream within the tolerance of its own exact fp32 filter, the
+    padding never written, the fp16 state exact."""
+    monkeypatch.setenv("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
+    sdrhip = built_lib
+    rng = np.random.default_rng(77)
+    ntaps, n, nstreams = 1024, 20000, 3
+    xs, ys = n + 72, n + 40  # x rows stay 16-B aligned (x_stride % 8 == 0)
+    h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
+    ns = ntaps - 1
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    sth = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(nstreams * ns, np.float16))
+    sentinel = np.float32(-12345.0)
+    y = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.full(nstreams * ys, sentinel, np.float32))
+    st_ref = [np.zeros(ns, np.float32) for _ in range(nstreams)]
+    for blk in range(2):
+        x = rng.standard_normal((nstreams, n)).astype(np.float32)
+        xp = np.zeros((nstreams, xs), np.float16)
+        xp[:, :n] = x.astype(np.float16)
+        d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, xp)
+        gpu_ctx.fir_block_f16_dev(d_x, n, nstreams, xs, d_h, ntaps, sth, ns, y, ys)
+        gpu_ctx.synchronize()
+        got = y.download().reshape(nstreams, ys)
+        assert np.all(got[:, n:] == sentinel), "padding written"
+        for s in range(nstreams):
+            want = oracle.fir_block(x[s], h, st_ref[s])
+            scale = np.abs(h).sum() * np.abs(x[s]).max()
+            assert np.abs(got[s, :n] - want).max() <= 2.0 ** -9 * scale, f"stream {s} block {blk}"
+        assert np.array_equal(sth.download(np.float16).reshape(nstreams, ns),
+                              x[:, -ns:].astype(np.float16)), "fp16 state"
+
+
 # ------------------------------------------------------- batched device API
 
 def _fm_streams(nstreams, n, seed=5):
