@@ -341,7 +341,8 @@ struct MfArgs {
   long long y_stride;
   int wg_per_stream;
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
-  int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA
+  int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
+                          // 3 = no tap staging
 };
 
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
@@ -381,10 +382,11 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   _Float16* hb = hcp + 8 * a.lc;
   const int nhb = a.lc + 40;
   float hv[kMfTaps];
+  const int ntl = a.ablate == 3 ? 0 : a.ntaps;  // (ablation 3: no tap loads, no copies)
 #pragma unroll
   for (int k = 0; k < kMfTaps; ++k) {
     const int v = tid + k * kNT - 32;
-    hv[k] = (v >= 0 && v < a.ntaps) ? a.h[a.ntaps - 1 - v] : 0.0f;
+    hv[k] = (v >= 0 && v < ntl) ? a.h[a.ntaps - 1 - v] : 0.0f;
   }
 #pragma unroll
   for (int k = 0; k < kMfChunks; ++k) {
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   if (m0 == 0)
     for (int i = tid; i < a.ns; i += 64 * kMfWaves) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
   const int cpr = a.lc >> 3;  // 16-B chunks per copy
-  for (int c = tid; c < 8 * cpr; c += 64 * kMfWaves) {
+  for (int c = tid; c < (a.ablate == 3 ? 0 : 8 * cpr); c += 64 * kMfWaves) {
     const int q = c / cpr, w0 = 8 * (c - q * cpr);
     half8 v;
 #pragma unroll
