@@ -316,6 +316,12 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
 #ifndef SDR_LP_EARLY
 #define SDR_LP_EARLY 1
 #endif
+// SDR_LP_NT: the items' LDS-DMA with the non-temporal policy (each input is
+// read once; MI355X_MICROARCH.md's nt-weights row: issued -> landed -18 %):
+// cfg3 0.1171-0.1192 vs 0.1170-0.1202 ms, neutral (profiles/r04f/), off
+#ifndef SDR_LP_NT
+#define SDR_LP_NT 0
+#endif
 constexpr int kLpWaves = 7;
 constexpr int kLpSlots = 64 * kLpWaves;
 constexpr int kLpGroups = kLpSlots / 16;
@@ -462,7 +468,7 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
     // lanes of one instruction are consecutive chunks
     for (int j0 = (int)(jlo & ~63LL) + wv * 64; j0 < jhi; j0 += 64 * nwv) {
       const int j = j0 + ln;
-      if (j >= jlo && j < jhi) __builtin_amdgcn_global_load_lds(xs + P0 + 4LL * j, buf + 4 * j0, 16, 0, 0);
+      if (j >= jlo && j < jhi) __builtin_amdgcn_global_load_lds(xs + P0 + 4LL * j, buf + 4 * j0, 16, 0, SDR_LP_NT ? 2 : 0);
     }
   };
   // DMA_FIRST (the loader wave, which waits for nothing else): the span's
