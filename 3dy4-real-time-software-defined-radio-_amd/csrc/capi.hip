@@ -1062,24 +1062,44 @@ int sdr_stereo_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, 
                                st->ns_bpf, w->pilot, w->dstride);
 }
 
-// PLL recurrence (:123-126), NCO x stereo band (:127), stereo resampler
-// (:129), L/R + interleave + s16 (:131-132, 304-314)
-int sdr_stereo_back_dev(sdr_ctx* c, float audio_fs, const sdr_stereo_taps* taps, sdr_stereo_state* st,
-                        sdr_stereo_work* w, int16_t* pcm, long long pcm_stride) {
+// PLL recurrence (:123-126): the block's oscillator arguments into the work
+int sdr_stereo_pll_dev(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_stereo_work* w) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!st || !w) return fail(c, SDR_EINVAL, "null state / work");
+  hipError_t e = sdr::launch_pll_recurrence(w->pilot, w->nd, w->nstreams, w->dstride, 19e3f, audio_fs, 2.0f, 0.0f,
+                                            0.01f, st->pll, w->args, w->pstride, c->cur, w->guard);
+  if (e != hipSuccess) return hip_fail(c, e, "pll launch");
+  return SDR_OK;
+}
+
+// NCO x stereo band (:127), stereo resampler (:129), L/R + interleave + s16
+// (:131-132, 304-314)
+int sdr_stereo_post_dev(sdr_ctx* c, const sdr_stereo_taps* taps, sdr_stereo_state* st, sdr_stereo_work* w,
+                        int16_t* pcm, long long pcm_stride) {
   int rc = enter(c);
   if (rc) return rc;
   if (!taps || !st || !w || !pcm) return fail(c, SDR_EINVAL, "null taps / state / work / pcm");
   const int n = w->nstreams;
   if (n > 1 && pcm_stride < 2 * w->na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
-  hipError_t e = sdr::launch_pll_recurrence(w->pilot, w->nd, n, w->dstride, 19e3f, audio_fs, 2.0f, 0.0f, 0.01f,
-                                            st->pll, w->args, w->pstride, c->cur, w->guard);
-  if (e != hipSuccess) return hip_fail(c, e, "pll launch");
-  e = sdr::launch_nco(w->args, w->pstride, w->nd, n, 2.0f, 0.0f, w->sband, w->dstride, w->mixed, w->dstride, c->cur);
+  hipError_t e =
+      sdr::launch_nco(w->args, w->pstride, w->nd, n, 2.0f, 0.0f, w->sband, w->dstride, w->mixed, w->dstride, c->cur);
   if (e != hipSuccess) return hip_fail(c, e, "nco launch");
   if ((rc = sdr_resample_f32_dev(c, w->up, w->down, w->mixed, w->nd, n, w->dstride, taps->h_audio, taps->audio_taps,
                                  st->stereo_lp_state, st->ns_audio, w->slp, w->astride)))
     return rc;
   return sdr_stereo_pcm_dev(c, w->mono, w->slp, w->na, n, w->astride, pcm, pcm_stride);
+}
+
+// the PLL stage and the post stage in one call on this context's stream
+int sdr_stereo_back_dev(sdr_ctx* c, float audio_fs, const sdr_stereo_taps* taps, sdr_stereo_state* st,
+                        sdr_stereo_work* w, int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!taps || !st || !w || !pcm) return fail(c, SDR_EINVAL, "null taps / state / work / pcm");
+  if (w->nstreams > 1 && pcm_stride < 2 * w->na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
+  if ((rc = sdr_stereo_pll_dev(c, audio_fs, st, w))) return rc;
+  return sdr_stereo_post_dev(c, taps, st, w, pcm, pcm_stride);
 }
 
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

@@ -108,6 +108,8 @@ _SIGS = {
     "sdr_stereo_work_destroy": [_vp, _vp],
     "sdr_stereo_front_u8_dev": [_vp, _vp, _ll, _vp, _vp, _vp],
     "sdr_stereo_back_dev": [_vp, C.c_float, _vp, _vp, _vp, _vp, _ll],
+    "sdr_stereo_pll_dev": [_vp, C.c_float, _vp, _vp],
+    "sdr_stereo_post_dev": [_vp, _vp, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
 }
@@ -495,6 +497,15 @@ class Context:
         """Front stage of the stereo path (src/project.cpp:72-121) into `work`."""
         self._check(lib().sdr_stereo_front_u8_dev(self._c, _ptr(iq), iq_stride, C.addressof(taps),
                                                   C.addressof(state), work._w), "stereo_front_u8_dev")
+
+    def stereo_pll_dev(self, audio_fs, state, work):
+        """sdr_stereo_pll_dev: the back stage's PLL recurrence only."""
+        self._check(lib().sdr_stereo_pll_dev(self._c, audio_fs, C.addressof(state), work._w), "stereo_pll_dev")
+
+    def stereo_post_dev(self, taps, state, work, pcm, pcm_stride):
+        """sdr_stereo_post_dev: NCO x stereo band, stereo resampler, L/R s16."""
+        self._check(lib().sdr_stereo_post_dev(self._c, C.addressof(taps), C.addressof(state), work._w, _ptr(pcm),
+                                              pcm_stride), "stereo_post_dev")
 
     def stereo_back_dev(self, audio_fs, taps, state, work, pcm, pcm_stride):
         """Back stage (PLL recurrence onwards, :123-132 + 304-314) from `work` to s16 L/R."""

@@ -323,6 +323,15 @@ int sdr_stereo_front_u8_dev(sdr_ctx *ctx, const uint8_t *iq, long long iq_stride
                             sdr_stereo_state *state, sdr_stereo_work *work);
 int sdr_stereo_back_dev(sdr_ctx *ctx, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
                         sdr_stereo_work *work, int16_t *pcm, long long pcm_stride);
+/* sdr_stereo_back_dev as two stages (a three-stage pipeline: block b+1's
+ * recurrence needs block b's PLL state only, not its post stage):
+ * sdr_stereo_pll_dev the recurrence (src/project.cpp:123-126, state->pll),
+ * sdr_stereo_post_dev NCO x stereo band, stereo resampler, L/R s16
+ * (:127-132, 304-314; state->stereo_lp_state).  Each stage's state is its
+ * own, so each may run on its own context's stream, ordered by events. */
+int sdr_stereo_pll_dev(sdr_ctx *ctx, float audio_fs, sdr_stereo_state *state, sdr_stereo_work *work);
+int sdr_stereo_post_dev(sdr_ctx *ctx, const sdr_stereo_taps *taps, sdr_stereo_state *state, sdr_stereo_work *work,
+                        int16_t *pcm, long long pcm_stride);
 
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the

@@ -340,21 +340,25 @@ def test_long_stream_segments_two_threads(built_lib, oracle, D, T, ns):
     assert_bits(res[1][3], pv, "prev vs the oracle")
 
 
+@pytest.mark.parametrize("stages", [2, 3])
 @pytest.mark.parametrize("graph", [False, True])
-def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
+def test_stereo_two_stage_pipeline(built_lib, oracle, graph, stages):
     """bench.py --stereo-pipeline's schedule (and sdr_project's): each block as
     sdr_stereo_front_u8_dev on one context's stream and sdr_stereo_back_dev on
     a second context's, two work objects in a ring, front(b) waiting for
     back(b-2) and back(b) for front(b) by sdr_ctx_wait_event -- block b+1's
     front overlapping block b's PLL recurrence.  128 streams x 5 mode-0
     blocks, direct or captured as one HIP graph spanning both streams:
-    every PCM byte and every carried state word against the oracle chain."""
+    every PCM byte and every carried state word against the oracle chain.
+    stages = 3: the back stage cut again after the recurrence
+    (sdr_stereo_pll_dev | sdr_stereo_post_dev on a third context), three
+    work objects in the ring -- bench.py --stereo-pipeline 2."""
     sdrhip = built_lib
     mode, nstreams, nblk = 0, 128, 5
     rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
     npairs = block_bytes // 2
     na = sdrhip.resample_out_len(up, down, npairs // D)
-    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb:  # each on its own (non-blocking) HIP stream
+    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb, sdrhip.Context(0) as cc:  # each on its own HIP stream
         blocks = _synth_blocks(ca, sdrhip, nstreams, npairs, nblk, 777)
         A = sdrhip.DeviceArray
         d_taps = {k: A.from_numpy(ca, v) for k, v in taps.items()}
@@ -368,21 +372,30 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
                                    d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr,
                                    d_st["stereo"].ptr, 100, d_st["pll"].ptr)
         pcm = [A(ca, nstreams * 2 * na * 2) for _ in range(nblk)]
-        works = [ca.stereo_work(D, npairs, up, down, nstreams) for _ in range(2)]
-        ev_f = [sdrhip.Event(ca) for _ in range(2)]
-        ev_b = [sdrhip.Event(ca) for _ in range(2)]
+        ns_ = stages
+        works = [ca.stereo_work(D, npairs, up, down, nstreams) for _ in range(ns_)]
+        ev_f = [sdrhip.Event(ca) for _ in range(ns_)]
+        ev_p = [sdrhip.Event(ca) for _ in range(ns_)]
+        ev_b = [sdrhip.Event(ca) for _ in range(ns_)]
 
         def run(b0, k):
             for j in range(k):
-                b, slot = b0 + j, (b0 + j) % 2
-                if j >= 2:
+                b, slot = b0 + j, (b0 + j) % ns_
+                if j >= ns_:
                     ev_b[slot].wait(ca)
                 ca.stereo_front_u8_dev(blocks[b][0], 2 * npairs, t, state, works[slot])
                 ev_f[slot].record(ca)
                 ev_f[slot].wait(cb)
-                cb.stereo_back_dev(audio_fs, t, state, works[slot], pcm[b], 2 * na)
-                ev_b[slot].record(cb)
-            ev_b[(b0 + k - 1) % 2].wait(ca)
+                if stages == 3:
+                    cb.stereo_pll_dev(audio_fs, state, works[slot])
+                    ev_p[slot].record(cb)
+                    ev_p[slot].wait(cc)
+                    cc.stereo_post_dev(t, state, works[slot], pcm[b], 2 * na)
+                    ev_b[slot].record(cc)
+                else:
+                    cb.stereo_back_dev(audio_fs, t, state, works[slot], pcm[b], 2 * na)
+                    ev_b[slot].record(cb)
+            ev_b[(b0 + k - 1) % ns_].wait(ca)
 
         try:
             run(0, 1)  # sizes both contexts' scratch (no allocation may happen inside a capture)
@@ -394,6 +407,7 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
                 run(1, nblk - 1)
             ca.synchronize()
             cb.synchronize()
+            cc.synchronize()
             if graph:
                 g.close()
             ost = [_stereo_state0() for _ in range(nstreams)]
@@ -411,5 +425,5 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
         finally:
             for w in works:
                 w.close()
-            for e in ev_f + ev_b:
+            for e in ev_f + ev_p + ev_b:
                 e.close()
