@@ -68,6 +68,11 @@
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
+// SDR_SCAN_VCONST (timing builds only, wrong outputs): fir_tile_sc's scan
+// with a VGPR in place of the SGPR taps
+#ifndef SDR_SCAN_VCONST
+#define SDR_SCAN_VCONST 0
+#endif
 
 namespace sdr {
 namespace {
@@ -1096,6 +1101,16 @@ __device__ __forceinline__ void scan_one(const float* w, float (&acc)[R], const 
     for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
 #pragma unroll
     for (int i = 0; i < k1 - k0; ++i) asm volatile("" : "+s"(hs[i]));
+#if SDR_SCAN_VCONST
+    // timing ablation only (wrong outputs): every multiply of the pass takes
+    // one VGPR operand instead of its SGPR tap
+    float hvc[R];  // one per output, so no two products are the same value (no CSE)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      hvc[r] = hs[r];
+      asm volatile("" : "+v"(hvc[r]));
+    }
+#endif
     constexpr int wlo = G::HALO - (k1 - 1) > 0 ? G::HALO - (k1 - 1) : 0;
     constexpr int whi = G::HALO + D * (R - 1) - k0;
     constexpr int clo = wlo / 4, chi = whi / 4;
@@ -1113,10 +1128,15 @@ __device__ __forceinline__ void scan_one(const float* w, float (&acc)[R], const 
           constexpr int r = decltype(ri)::value;
           constexpr int k = G::HALO + D * r - (4 * c + j);
           if constexpr (k >= k0 && k < k1) {
+#if SDR_SCAN_VCONST
+            const float tap = hvc[r];
+#else
+            const float tap = hs[k - k0];
+#endif
             if constexpr (FMA)
-              acc[r] = __builtin_fmaf(hs[k - k0], e[j], acc[r]);
+              acc[r] = __builtin_fmaf(tap, e[j], acc[r]);
             else
-              acc[r] = acc[r] + hs[k - k0] * e[j];
+              acc[r] = acc[r] + tap * e[j];
           }
         });
       });
