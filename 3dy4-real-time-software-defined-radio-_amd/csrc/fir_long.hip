@@ -343,6 +343,7 @@ struct MfArgs {
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
   int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
                           // 3 = no tap staging
+  int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
 };
 
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
@@ -388,17 +389,40 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     const int v = tid + k * kNT - 32;
     hv[k] = (v >= 0 && v < ntl) ? a.h[a.ntaps - 1 - v] : 0.0f;
   }
+  // the stream's first workgroup (pb = -T, T <= 4096 = kMfSt * kNT): the
+  // carried state for image positions q in [-T, 0) and the new state (the
+  // block's last ns inputs, src/filter.cpp:82) join the same load batch, so
+  // this workgroup waits out one memory latency like the others, not three
+  constexpr int kMfSt = 16;
+  const bool head = a.head_pre && pb < 0;
+  _Float16 sv[kMfSt], nv[kMfSt];
+  if (head) {
+#pragma unroll
+    for (int k = 0; k < kMfSt; ++k) {
+      const int q = (int)pb + tid + k * kNT;
+      sv[k] = (q < 0 && q >= -a.ns) ? st[a.ns + q] : (_Float16)0;
+      const int i = tid + k * kNT;
+      nv[k] = i < a.ns ? xs[a.n - a.ns + i] : (_Float16)0;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kMfChunks; ++k) {
     const int c = tid + k * kNT;
-    if (c < nchunk) *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
+    if (c < nchunk && !(head && pb + 8LL * c < 0)) *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
+  }
+  if (head) {
+#pragma unroll
+    for (int k = 0; k < kMfSt; ++k) {
+      const int q = (int)pb + tid + k * kNT;
+      if (q < 0) img[mf_pad(q - (int)pb)] = sv[k];
+    }
   }
   // block edges (the stream's first and last workgroups), element-wise over
   // the clamped chunks: the carried state before 0, zeros past n
-  if (pb < 0 || pb + a.span > a.n) {
+  if ((pb < 0 && !head) || pb + a.span > a.n) {
     for (int c = tid; c < nchunk; c += kNT) {
       const long long p = pb + 8LL * c;
-      if (p >= 0 && p + 8 <= a.n) continue;
+      if ((p >= 0 || head) && p + 8 <= a.n) continue;
       _Float16* d = img + mf_pad(8 * c);
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
@@ -414,8 +438,14 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // the stream's first workgroup is the only reader of the old state (staged
   // above): it writes the new one, the block's last ns inputs
   // (src/filter.cpp:82), after that barrier
-  if (m0 == 0)
-    for (int i = tid; i < a.ns; i += 64 * kMfWaves) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
+  if (head) {
+#pragma unroll
+    for (int k = 0; k < kMfSt; ++k)
+      if (tid + k * kNT < a.ns) a.state[(long long)s * a.ns + tid + k * kNT] = nv[k];
+    for (int i = tid + kMfSt * kNT; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
+  } else if (m0 == 0) {
+    for (int i = tid; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
+  }
   const int cpr = a.lc >> 3;  // 16-B chunks per copy
   for (int c = tid; c < (a.ablate == 3 ? 0 : 8 * cpr); c += 64 * kMfWaves) {
     const int q = c / cpr, w0 = 8 * (c - q * cpr);
@@ -544,6 +574,8 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.span = kMfOut + a.kd - 32;
     static const int ablate = env_int("SDR_ABLATE", 0);
     a.ablate = ablate;
+    static const int head_pre = env_int("SDR_F16_HEAD", 1);
+    a.head_pre = head_pre;
     // image, 8 tap copies, the reversed taps (a.lc + 40 halves)
     const size_t lds = ((size_t)mf_pad(a.span) + 8 + 9 * (size_t)a.lc + 40) * sizeof(_Float16);
     const long long blocks = (long long)a.wg_per_stream * nstreams;

@@ -345,6 +345,38 @@ def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, monkeypatch, kern
                               x[:, -ns:].astype(np.float16)), "fp16 state"
 
 
+@pytest.mark.parametrize("head", ["1", "0"])
+@pytest.mark.parametrize("ns", [1500, 5000])
+def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, monkeypatch, ns, head):
+    """The MFMA fp16 arm with a carried state longer than T-1 (the first
+    workgroup stages positions [-T, 0) of it and rewrites all ns, past 4,096
+    through its loop), under both state-staging orders (SDR_F16_HEAD), two
+    blocks: within the tolerance of the exact fp32 filter, the state exact."""
+    monkeypatch.setenv("SDR_F16_MFMA", "1")
+    monkeypatch.setenv("SDR_F16_HEAD", head)
+    sdrhip = built_lib
+    rng = np.random.default_rng(ns)
+    ntaps, n, nstreams = 1024, 20000, 2
+    h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    st0 = rng.standard_normal((nstreams, ns)).astype(np.float16)
+    sth = sdrhip.DeviceArray.from_numpy(gpu_ctx, st0.reshape(-1))
+    st_ref = [st0[s].astype(np.float32) for s in range(nstreams)]
+    y = sdrhip.DeviceArray(gpu_ctx, nstreams * n * 4)
+    for blk in range(2):
+        x = rng.standard_normal((nstreams, n)).astype(np.float16).astype(np.float32)
+        xh = sdrhip.DeviceArray.from_numpy(gpu_ctx, x.astype(np.float16))
+        gpu_ctx.fir_block_f16_dev(xh, n, nstreams, n, d_h, ntaps, sth, ns, y, n)
+        gpu_ctx.synchronize()
+        got = y.download().reshape(nstreams, n)
+        for s in range(nstreams):
+            want = oracle.fir_block(x[s], h, st_ref[s])
+            scale = np.abs(h).sum() * max(np.abs(x[s]).max(), 4.0)
+            assert np.abs(got[s] - want).max() <= 2.0 ** -9 * scale, f"stream {s} block {blk}"
+        assert np.array_equal(sth.download(np.float16).reshape(nstreams, ns),
+                              x[:, -ns:].astype(np.float16)), "fp16 state"
+
+
 # ------------------------------------------------------- batched device API
 
 def _fm_streams(nstreams, n, seed=5):
