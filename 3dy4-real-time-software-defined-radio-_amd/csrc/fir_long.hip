@@ -342,7 +342,7 @@ struct MfArgs {
   int wg_per_stream;
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
   int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
-                          // 3 = no tap staging
+                          // 3 = no tap staging, 4 = no output stores
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
 };
 
@@ -504,6 +504,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     for (int g = 0; g < 4; ++g) {
       const long long m = m0 + tb0 + t * 1024 + 32 * i + 8 * g + 4 * hh;
       const float4 v = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+      if (a.ablate == 4 && v.x != -0x1.234p100f) continue;  // (ablation 4: no stores)
       if (m + 4 <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
         *reinterpret_cast<float4*>(ys + m) = v;
       } else {
