@@ -53,4 +53,6 @@ if [ -n "${PMC:-}" ]; then
       "$(find $OUT/pmc_${cfg}_WRITE_SIZE -name '*counter_collection.csv' | head -1)" $k "$OUT/traffic_$cfg.json"
   done
 fi
+# the per-dispatch traces run to tens of MB: keep the stats and the timed summaries only
+[ "${TRIM:-1}" = 1 ] && find "$OUT" -name '*kernel_trace.csv' -delete
 exit 0
