@@ -326,9 +326,7 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // the default: cfg5h 0.0161-0.0163 vs 0.0427-0.0428 ms on the dot2 kernel
 // (profiles/r04e/ab.txt); SDR_F16_MFMA=0 selects v_dot2
 constexpr int kF16MfmaDefault = 1;
-constexpr int kMfNT = 2;                      // 1,024-output tiles per wave
-constexpr int kMfWaves = 4;                   // one wave per SIMD
-constexpr int kMfOut = 1024 * kMfNT * kMfWaves;  // outputs per workgroup
+constexpr int kMfOut = 8192;                  // outputs per workgroup: 8 tiles of 1,024
 
 struct MfArgs {
   const _Float16* x;
@@ -348,7 +346,10 @@ struct MfArgs {
 
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
 
+// kMfWaves waves (4: one per SIMD, two tiles each; 8: two per SIMD, one tile each)
+template <int kMfWaves>
 __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
+  constexpr int kMfNT = 8 / kMfWaves;           // 1,024-output tiles per wave
   typedef _Float16 half8 __attribute__((ext_vector_type(8)));
   typedef float f16x __attribute__((ext_vector_type(16)));
   extern __shared__ __attribute__((aligned(16))) _Float16 mf_lds[];
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // load-then-store loop waits out one memory latency per iteration.
   // kMfChunks covers the image at T <= 4096 (span <= 12,288 halves) and
   // kMfTaps the reversed taps (a.lc + 40 <= 4,264 halves).
-  constexpr int kNT = 64 * kMfWaves, kMfChunks = 6, kMfTaps = 17;
+  constexpr int kNT = 64 * kMfWaves, kMfChunks = (kMfOut + 4096) / (8 * kNT), kMfTaps = (4264 + kNT - 1) / kNT;
   const int nchunk = a.span >> 3;
   // every register defined (clamped, in-bounds addresses: n >= 8 on this
   // path), so the array stays in VGPRs; the edge chunks are rewritten below
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // carried state for image positions q in [-T, 0) and the new state (the
   // block's last ns inputs, src/filter.cpp:82) join the same load batch, so
   // this workgroup waits out one memory latency like the others, not three
-  constexpr int kMfSt = 16;
+  constexpr int kMfSt = 4096 / kNT;
   const bool head = a.head_pre && pb < 0;
   _Float16 sv[kMfSt], nv[kMfSt];
   if (head) {
@@ -575,14 +576,20 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.span = kMfOut + a.kd - 32;
     static const int ablate = env_int("SDR_ABLATE", 0);
     a.ablate = ablate;
-    static const int head_pre = env_int("SDR_F16_HEAD", 1);
+    const int head_pre = env_int("SDR_F16_HEAD", 1);  // (read per launch: the tests switch it)
     a.head_pre = head_pre;
     // image, 8 tap copies, the reversed taps (a.lc + 40 halves)
     const size_t lds = ((size_t)mf_pad(a.span) + 8 + 9 * (size_t)a.lc + 40) * sizeof(_Float16);
     const long long blocks = (long long)a.wg_per_stream * nstreams;
     if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
     // one launch: each stream's first workgroup commits the state itself
-    hipLaunchKernelGGL(fir_long_mfma, dim3((unsigned)blocks), dim3(64 * kMfWaves), lds, st, a);
+    // two waves per SIMD, one tile each: 8.8 vs 10.9 us per kernel on cfg5h
+    // (profiles/r04y/); SDR_F16_W8=0 restores four waves of two tiles
+    const int w8 = env_int("SDR_F16_W8", 1);
+    if (w8)
+      hipLaunchKernelGGL(fir_long_mfma<8>, dim3((unsigned)blocks), dim3(512), lds, st, a);
+    else
+      hipLaunchKernelGGL(fir_long_mfma<4>, dim3((unsigned)blocks), dim3(256), lds, st, a);
     return hipGetLastError();
   }
   const int len = (int)fir_long_h_pairs(ntaps);

@@ -345,15 +345,19 @@ def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, monkeypatch, kern
                               x[:, -ns:].astype(np.float16)), "fp16 state"
 
 
+@pytest.mark.parametrize("waves", ["8", "4"])
 @pytest.mark.parametrize("head", ["1", "0"])
 @pytest.mark.parametrize("ns", [1500, 5000])
-def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, monkeypatch, ns, head):
+def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, monkeypatch, ns, head, waves):
     """The MFMA fp16 arm with a carried state longer than T-1 (the first
-    workgroup stages positions [-T, 0) of it and rewrites all ns, past 4,096
-    through its loop), under both state-staging orders (SDR_F16_HEAD), two
-    blocks: within the tolerance of the exact fp32 filter, the state exact."""
+    workgroup stages positions [-T, 0) of it and rewrites all ns, past its
+    register slots through its loop), under both state-staging orders
+    (SDR_F16_HEAD) and both workgroup shapes (SDR_F16_W8: 8 waves of one tile,
+    4 of two), two blocks: within the tolerance of the exact fp32 filter, the
+    state exact."""
     monkeypatch.setenv("SDR_F16_MFMA", "1")
     monkeypatch.setenv("SDR_F16_HEAD", head)
+    monkeypatch.setenv("SDR_F16_W8", "1" if waves == "8" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(ns)
     ntaps, n, nstreams = 1024, 20000, 2
