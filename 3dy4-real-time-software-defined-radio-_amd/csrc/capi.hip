@@ -208,6 +208,38 @@ int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
+
+namespace {
+struct SwitchDef {
+  const char* name;
+  int dflt;
+};
+// the measured defaults (DESIGN.md 5.2 lists the A/Bs behind each)
+constexpr SwitchDef kSwitchDefs[kSwCount] = {
+    {"SDR_FIR_SC", 1},          {"SDR_FIR_SC_U8", 1},    {"SDR_RESAMPLE_LP", 1}, {"SDR_RESAMPLE_LOADER", 1},
+    {"SDR_RESAMPLE_RS", 1},     {"SDR_RESAMPLE_PP", 1},  {"SDR_LONG_VTAP", 1},   {"SDR_F16_MFMA", 1},
+    {"SDR_F16_HEAD", 1},        {"SDR_F16_W8", 1},       {"SDR_PLL_FAST", 1},    {"SDR_PLL_GUARD", 1}};
+std::atomic<int> g_switch[kSwCount];
+std::once_flag g_switch_once;
+
+void switches_init() {
+  std::call_once(g_switch_once, [] {
+    for (int i = 0; i < kSwCount; ++i) g_switch[i].store(env_int(kSwitchDefs[i].name, kSwitchDefs[i].dflt));
+  });
+}
+
+int switch_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < kSwCount; ++i)
+    if (std::strcmp(name, kSwitchDefs[i].name) == 0) return i;
+  return -1;
+}
+}  // namespace
+
+int sw(Switch s) {
+  switches_init();
+  return g_switch[s].load(std::memory_order_relaxed);
+}
 }  // namespace sdr
 
 extern "C" {
@@ -223,6 +255,21 @@ const char* sdr_strerror(int code) {
     case SDR_ENODEV: return "no such device";
     default: return "unknown error";
   }
+}
+
+int sdr_set_switch(const char* name, int value) {
+  const int i = sdr::switch_index(name);
+  if (i < 0) return SDR_EINVAL;
+  sdr::switches_init();
+  sdr::g_switch[i].store(value, std::memory_order_relaxed);
+  return SDR_OK;
+}
+
+int sdr_get_switch(const char* name, int* value) {
+  const int i = sdr::switch_index(name);
+  if (i < 0 || !value) return SDR_EINVAL;
+  *value = sdr::sw(static_cast<sdr::Switch>(i));
+  return SDR_OK;
 }
 
 int sdr_device_count(int* count) {
@@ -675,14 +722,43 @@ static int resample_dev(sdr_ctx* c, int up, int down, const float* x, long long 
   return SDR_OK;
 }
 
+// The streams that used a device object (a resample plan's tables, a stereo
+// work's buffers): one event per stream, recorded after each direct launch
+// that reads or writes the object (and after the plan's table build), so
+// destroy waits for exactly that work -- on whichever contexts' streams it
+// was enqueued -- before freeing.  Launches recorded into a graph are not
+// seen: the graph's replays must have completed before destroy (sdr_hip.h).
+struct StreamUses {
+  std::mutex mu;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> v;
+  hipError_t mark(hipStream_t s) {
+    if (capturing(s)) return hipSuccess;
+    std::lock_guard<std::mutex> lk(mu);
+    hipEvent_t ev = nullptr;
+    for (auto& u : v)
+      if (u.first == s) ev = u.second;
+    if (!ev) {
+      const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+      v.emplace_back(s, ev);
+    }
+    return hipEventRecord(ev, s);
+  }
+  void wait_and_release() {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& u : v) {
+      (void)hipEventSynchronize(u.second);
+      (void)hipEventDestroy(u.second);
+    }
+    v.clear();
+  }
+};
+
 struct sdr_resample_plan {
   int up = 0, down = 0, ntaps = 0;
   const float* h = nullptr;
   float* tables = nullptr;  // resample_lp's tables, or nullptr when the shape takes another kernel
-  // one event per stream that launched with the tables (recorded after each
-  // direct launch): destroy waits for exactly those, not the whole device
-  std::mutex mu;
-  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  StreamUses uses;          // the table build and every direct launch with the tables
 };
 
 int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int ntaps, sdr_resample_plan** out) {
@@ -710,9 +786,10 @@ int sdr_resample_plan_create(sdr_ctx* c, int up, int down, const float* h, int n
       (void)hipFree(p->tables);
       delete p;
       return hip_fail(c, e, "resample plan tables");
-    } else if ((e = hipStreamSynchronize(c->cur)) != hipSuccess) {
+    } else if ((e = hipStreamSynchronize(c->cur)) != hipSuccess || (e = p->uses.mark(c->cur)) != hipSuccess) {
       // built before the plan is handed out: a later call may run on
-      // another stream (sdr_ctx_set_stream), which nothing would order
+      // another stream (sdr_ctx_set_stream), which nothing would order;
+      // the build is recorded as a use of the plan too
       (void)hipFree(p->tables);
       delete p;
       return hip_fail(c, e, "resample plan tables");
@@ -726,15 +803,10 @@ int sdr_resample_plan_destroy(sdr_ctx* c, sdr_resample_plan* p) {
   int rc = enter(c);
   if (rc) return rc;
   if (p) {
-    if (p->tables) {
-      // every stream that used the plan, not only the current one (graphs
-      // recorded with the plan must be destroyed before it, sdr_hip.h)
-      for (auto& u : p->uses) {
-        (void)hipEventSynchronize(u.second);
-        (void)hipEventDestroy(u.second);
-      }
-      (void)hipFree(p->tables);
-    }
+    // every stream that used the plan, not only the current one (graph
+    // replays of calls with the plan must have completed, sdr_hip.h)
+    p->uses.wait_and_release();
+    if (p->tables) (void)hipFree(p->tables);
     delete p;
   }
   return SDR_OK;
@@ -745,17 +817,8 @@ int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const floa
   if (!p) return fail(c, SDR_EINVAL, "null plan");
   const int rc = resample_dev(c, p->up, p->down, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride,
                               p->tables);
-  if (rc || !p->tables || capturing(c->cur)) return rc;
-  auto* pm = const_cast<sdr_resample_plan*>(p);
-  std::lock_guard<std::mutex> lk(pm->mu);
-  hipEvent_t ev = nullptr;
-  for (auto& u : pm->uses)
-    if (u.first == c->cur) ev = u.second;
-  if (!ev) {
-    SDR_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    pm->uses.emplace_back(c->cur, ev);
-  }
-  SDR_HIP(c, hipEventRecord(ev, c->cur));
+  if (rc || !p->tables) return rc;
+  SDR_HIP(c, const_cast<sdr_resample_plan*>(p)->uses.mark(c->cur));
   return SDR_OK;
 }
 
@@ -985,6 +1048,7 @@ struct sdr_stereo_work {
   float *demod = nullptr, *delayed = nullptr, *mono = nullptr, *pilot = nullptr, *sband = nullptr, *slp = nullptr,
         *args = nullptr, *mixed = nullptr;
   uint8_t* guard = nullptr;
+  StreamUses uses;  // every stream a stage ran on (destroy waits for them)
 };
 
 int sdr_stereo_work_create(sdr_ctx* c, int D, long long npairs, int up, int down, int nstreams,
@@ -1031,7 +1095,9 @@ int sdr_stereo_work_destroy(sdr_ctx* c, sdr_stereo_work* w) {
   int rc = enter(c);
   if (rc) return rc;
   if (w) {
-    (void)hipStreamSynchronize(c->cur);  // the caller's last use is on this context's stream
+    // the stages may have run on other contexts' streams (the two-stage
+    // pipeline: front on one, back on another): wait for every one of them
+    w->uses.wait_and_release();
     (void)hipFree(w->mem);
     delete w;
   }
@@ -1046,26 +1112,30 @@ int sdr_stereo_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, 
   if (rc) return rc;
   if (!taps || !st || !w) return fail(c, SDR_EINVAL, "null taps / state / work");
   const int n = w->nstreams;
-  if ((rc = sdr_frontend_u8_dev(c, w->D, iq, w->npairs, n, iq_stride, taps->h_rf, taps->rf_taps, st->state_i,
-                                st->state_q, st->ns_rf, st->prev_i, st->prev_q, w->demod, w->dstride)))
-    return rc;
-  if ((rc = sdr_delay_f32_dev(c, w->demod, w->nd, n, w->dstride, st->delay_state, st->ns_delay, w->delayed,
-                              w->dstride)))
-    return rc;
-  if ((rc = sdr_resample_f32_dev(c, w->up, w->down, w->delayed, w->nd, n, w->dstride, taps->h_audio,
-                                 taps->audio_taps, st->state_audio, st->ns_audio, w->mono, w->astride)))
-    return rc;
-  if ((rc = sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_stereo, taps->bpf_taps,
-                                  st->stereo_state, st->ns_bpf, w->sband, w->dstride)))
-    return rc;
-  return sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_pilot, taps->bpf_taps, st->pilot_state,
+  rc = sdr_frontend_u8_dev(c, w->D, iq, w->npairs, n, iq_stride, taps->h_rf, taps->rf_taps, st->state_i,
+                           st->state_q, st->ns_rf, st->prev_i, st->prev_q, w->demod, w->dstride);
+  if (!rc)
+    rc = sdr_delay_f32_dev(c, w->demod, w->nd, n, w->dstride, st->delay_state, st->ns_delay, w->delayed, w->dstride);
+  if (!rc)
+    rc = sdr_resample_f32_dev(c, w->up, w->down, w->delayed, w->nd, n, w->dstride, taps->h_audio, taps->audio_taps,
+                              st->state_audio, st->ns_audio, w->mono, w->astride);
+  if (!rc)
+    rc = sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_stereo, taps->bpf_taps, st->stereo_state,
+                               st->ns_bpf, w->sband, w->dstride);
+  if (!rc)
+    rc = sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_pilot, taps->bpf_taps, st->pilot_state,
                                st->ns_bpf, w->pilot, w->dstride);
+  // marked even after a failed launch: whatever was enqueued uses the work
+  const hipError_t e = w->uses.mark(c->cur);
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  return SDR_OK;
 }
 
-// PLL recurrence (:123-126): the block's oscillator arguments into the work
-int sdr_stereo_pll_dev(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_stereo_work* w) {
-  int rc = enter(c);
-  if (rc) return rc;
+// PLL recurrence (:123-126): the block's oscillator arguments into the work.
+// (A three-stage split -- recurrence | post stage on a third context -- was
+// measured slower than two stages and is not part of the ABI)
+static int stereo_pll(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_stereo_work* w) {
   if (!st || !w) return fail(c, SDR_EINVAL, "null state / work");
   hipError_t e = sdr::launch_pll_recurrence(w->pilot, w->nd, w->nstreams, w->dstride, 19e3f, audio_fs, 2.0f, 0.0f,
                                             0.01f, st->pll, w->args, w->pstride, c->cur, w->guard);
@@ -1075,10 +1145,9 @@ int sdr_stereo_pll_dev(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_ste
 
 // NCO x stereo band (:127), stereo resampler (:129), L/R + interleave + s16
 // (:131-132, 304-314)
-int sdr_stereo_post_dev(sdr_ctx* c, const sdr_stereo_taps* taps, sdr_stereo_state* st, sdr_stereo_work* w,
-                        int16_t* pcm, long long pcm_stride) {
-  int rc = enter(c);
-  if (rc) return rc;
+static int stereo_post(sdr_ctx* c, const sdr_stereo_taps* taps, sdr_stereo_state* st, sdr_stereo_work* w,
+                       int16_t* pcm, long long pcm_stride) {
+  int rc = SDR_OK;
   if (!taps || !st || !w || !pcm) return fail(c, SDR_EINVAL, "null taps / state / work / pcm");
   const int n = w->nstreams;
   if (n > 1 && pcm_stride < 2 * w->na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
@@ -1098,8 +1167,12 @@ int sdr_stereo_back_dev(sdr_ctx* c, float audio_fs, const sdr_stereo_taps* taps,
   if (rc) return rc;
   if (!taps || !st || !w || !pcm) return fail(c, SDR_EINVAL, "null taps / state / work / pcm");
   if (w->nstreams > 1 && pcm_stride < 2 * w->na) return fail(c, SDR_EINVAL, "pcm stride < 2 x audio samples per block");
-  if ((rc = sdr_stereo_pll_dev(c, audio_fs, st, w))) return rc;
-  return sdr_stereo_post_dev(c, taps, st, w, pcm, pcm_stride);
+  rc = stereo_pll(c, audio_fs, st, w);
+  if (!rc) rc = stereo_post(c, taps, st, w, pcm, pcm_stride);
+  const hipError_t e = w->uses.mark(c->cur);  // marked even after a failed launch
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  return SDR_OK;
 }
 
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,

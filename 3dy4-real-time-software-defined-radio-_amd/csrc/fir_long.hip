@@ -16,6 +16,8 @@
 // the pass body is unrolled once and looped at run time.  At R = 4 a pass
 // is 256 multiplies/adds per lane against 10 LDS reads: VALU-bound, the
 // bound of this config (4,096 FLOP per IQ pair).
+#include <algorithm>
+
 #include "sdr_common.hpp"
 
 #pragma clang fp contract(off)
@@ -178,13 +180,21 @@ hipError_t launch_fir_long(const FirLaunch& f, const float* h, hipStream_t st) {
   a.img = a.halo + OUT_WG + 4;
   const long long blocks = (long long)a.tiles_per_stream * f.nstreams;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  // SDR_LONG_VTAP=0: SGPR taps (A/B; read per launch).  The tap copy needs
-  // 16-B aligned taps (ntaps is a multiple of 32).
-  if (env_int("SDR_LONG_VTAP", 1) != 0 && (reinterpret_cast<uintptr_t>(h) & 15) == 0)
-    hipLaunchKernelGGL(fir_long<1>, dim3((unsigned)blocks), dim3(64 * kLongNW),
-                       (size_t)(a.img + f.ntaps) * sizeof(float), st, a);
+  // LDS-staged taps (switch SDR_LONG_VTAP, measured at T = 1024) need 16-B
+  // aligned taps (ntaps is a multiple of 32) and ntaps*4 more LDS per
+  // workgroup; where that extra LDS would cut the workgroups a CU can hold
+  // below both 8 (four waves per SIMD) and the SGPR kernel's count -- long
+  // taps, e.g. T = 8192: 69.7 vs 36.9 KiB, 2 vs 4 per CU -- the SGPR-tap
+  // kernel runs.  Same bits either way.
+  const size_t lds_s = (size_t)a.img * sizeof(float), lds_v = lds_s + (size_t)f.ntaps * sizeof(float);
+  const size_t lds_cu = (size_t)device_lds_bytes();
+  if (lds_s > lds_cu) return hipErrorInvalidConfiguration;
+  const bool vtap = sw(kSwLongVtap) != 0 && (reinterpret_cast<uintptr_t>(h) & 15) == 0 && lds_v <= lds_cu &&
+                    lds_cu / lds_v >= std::min<size_t>(8, lds_cu / lds_s);
+  if (vtap)
+    hipLaunchKernelGGL(fir_long<1>, dim3((unsigned)blocks), dim3(64 * kLongNW), lds_v, st, a);
   else
-    hipLaunchKernelGGL(fir_long<0>, dim3((unsigned)blocks), dim3(64 * kLongNW), (size_t)a.img * sizeof(float), st, a);
+    hipLaunchKernelGGL(fir_long<0>, dim3((unsigned)blocks), dim3(64 * kLongNW), lds_s, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || f.ns <= 0) return e;
   hipLaunchKernelGGL(long_commit, dim3((f.ns + kWG - 1) / kWG, (unsigned)f.nstreams), dim3(kWG), 0, st, f.x0, f.n,
@@ -324,8 +334,7 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // Same operands as the dot2 kernel (fp16 x, state and taps), fp32
 // accumulation inside the MFMA: the same tolerance contract.
 // the default: cfg5h 0.0161-0.0163 vs 0.0427-0.0428 ms on the dot2 kernel
-// (profiles/r04e/ab.txt); SDR_F16_MFMA=0 selects v_dot2
-constexpr int kF16MfmaDefault = 1;
+// (profiles/r04e/ab.txt); switch SDR_F16_MFMA=0 selects v_dot2
 constexpr int kMfOut = 8192;                  // outputs per workgroup: 8 tiles of 1,024
 
 struct MfArgs {
@@ -376,7 +385,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   for (int k = 0; k < kMfChunks; ++k) {
     long long p = pb + 8LL * (tid + k * kNT);
     p = p < 0 ? 0 : (p > a.n - 8 ? a.n - 8 : p);
-    if (a.ablate == 1) p = 0;  // (ablation 1: one cached chunk instead of the stream)
+    if (SDR_ABL(a.ablate) == 1) p = 0;  // (ablation 1: one cached chunk instead of the stream)
     iv[k] = *reinterpret_cast<const u32x4*>(xs + (p & ~7LL));
   }
   // the reversed f16 taps once, hb[j] = hr[j - 32], hr[v] = h[T-1-v]
@@ -384,7 +393,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   _Float16* hb = hcp + 8 * a.lc;
   const int nhb = a.lc + 40;
   float hv[kMfTaps];
-  const int ntl = a.ablate == 3 ? 0 : a.ntaps;  // (ablation 3: no tap loads, no copies)
+  const int ntl = SDR_ABL(a.ablate) == 3 ? 0 : a.ntaps;  // (ablation 3: no tap loads, no copies)
 #pragma unroll
   for (int k = 0; k < kMfTaps; ++k) {
     const int v = tid + k * kNT - 32;
@@ -448,7 +457,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     for (int i = tid; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
   }
   const int cpr = a.lc >> 3;  // 16-B chunks per copy
-  for (int c = tid; c < (a.ablate == 3 ? 0 : 8 * cpr); c += 64 * kMfWaves) {
+  for (int c = tid; c < (SDR_ABL(a.ablate) == 3 ? 0 : 8 * cpr); c += 64 * kMfWaves) {
     const int q = c / cpr, w0 = 8 * (c - q * cpr);
     half8 v;
 #pragma unroll
@@ -468,7 +477,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // G steps per group; the next group's 3 G fragments are read while this
   // group's 2 G MFMAs run (kd is a multiple of 32 G: an even group count)
   constexpr int G = 3;
-  const int ngrp = a.ablate == 2 ? 0 : a.kd / (16 * G);  // (ablation 2: no MFMA)
+  const int ngrp = SDR_ABL(a.ablate) == 2 ? 0 : a.kd / (16 * G);  // (ablation 2: no MFMA)
   half8 av[G], bv[G][kMfNT];
   auto fetch = [&](int g0, half8 (&aa)[G], half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -505,7 +514,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     for (int g = 0; g < 4; ++g) {
       const long long m = m0 + tb0 + t * 1024 + 32 * i + 8 * g + 4 * hh;
       const float4 v = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
-      if (a.ablate == 4 && v.x != -0x1.234p100f) continue;  // (ablation 4: no stores)
+      if (SDR_ABL(a.ablate) == 4 && v.x != -0x1.234p100f) continue;  // (ablation 4: no stores)
       if (m + 4 <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
         *reinterpret_cast<float4*>(ys + m) = v;
       } else {
@@ -548,7 +557,7 @@ __global__ __launch_bounds__(kWG) void f32_to_f16(const float* __restrict__ x, l
 // 106 KiB at 4096), and no workgroup but a stream's first reaches into the
 // state (T < kMfOut), which lets that one commit the new state in-kernel
 bool fir_f16_uses_mfma(int ntaps) {
-  return ntaps % 8 == 0 && ntaps <= 4096 && env_int("SDR_F16_MFMA", kF16MfmaDefault) != 0;
+  return ntaps % 8 == 0 && ntaps <= 4096 && sw(kSwF16Mfma) != 0;
 }
 
 size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32); }
@@ -574,9 +583,9 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.y_stride = y_stride;
     a.wg_per_stream = (int)((n + kMfOut - 1) / kMfOut);
     a.span = kMfOut + a.kd - 32;
-    static const int ablate = env_int("SDR_ABLATE", 0);
+    static const int ablate = SDR_TIMING_ENV("SDR_ABLATE", 0);
     a.ablate = ablate;
-    const int head_pre = env_int("SDR_F16_HEAD", 1);  // (read per launch: the tests switch it)
+    const int head_pre = sw(kSwF16Head);  // (switch: the tests run both orders)
     a.head_pre = head_pre;
     // image, 8 tap copies, the reversed taps (a.lc + 40 halves)
     const size_t lds = ((size_t)mf_pad(a.span) + 8 + 9 * (size_t)a.lc + 40) * sizeof(_Float16);
@@ -585,7 +594,7 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     // one launch: each stream's first workgroup commits the state itself
     // two waves per SIMD, one tile each: 8.8 vs 10.9 us per kernel on cfg5h
     // (profiles/r04y/); SDR_F16_W8=0 restores four waves of two tiles
-    const int w8 = env_int("SDR_F16_W8", 1);
+    const int w8 = sw(kSwF16W8);
     if (w8)
       hipLaunchKernelGGL(fir_long_mfma<8>, dim3((unsigned)blocks), dim3(512), lds, st, a);
     else

@@ -413,7 +413,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
   Stage sa0, sa1;
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.ablate != 1)
+  if (SDR_ABL(a.ablate) != 1)
     stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
 
   auto tile = [&](const int lin, Stage& v0, Stage& v1) __attribute__((always_inline)) {
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     }
     __syncthreads();
     SDR_TRACE_AT(2);
-    if (lin + step < last && a.ablate != 1)
+    if (lin + step < last && SDR_ABL(a.ablate) != 1)
       stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, lin + step), n, tid, v0, v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
       acc0[r] = 0.0f;
       acc1[r] = 0.0f;
     }
-    if (a.ablate == 2) {
+    if (SDR_ABL(a.ablate) == 2) {
       acc0[0] = lds0[lbase];
       acc1[0] = lds1[lbase];
     } else {
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
           constexpr int k0 = decltype(pi)::value * KP;
           constexpr int k1 = k0 + KP < T ? k0 + KP : T;
           // ablate 4 (timing only): one pass of three -- how much a cheaper scan buys
-          if (a.ablate == 4 && k0 > 0) return;
+          if (SDR_ABL(a.ablate) == 4 && k0 > 0) return;
 #pragma unroll
           for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
 #pragma unroll
@@ -788,7 +788,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
   Stage sa0, sa1;
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) sa0[i] = sa1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.ablate != 1)
+  if (SDR_ABL(a.ablate) != 1)
     stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, first), n, tid, sa0, sa1);
 
   // A tile's outputs wait in registers and are stored after the next tile's
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     SDR_TRACE_AT(2);
     const int next = nxt();
     if constexpr (SDR_FIR_DEFER) flush();  // the previous tile's outputs
-    if (next >= 0 && a.ablate != 1)
+    if (next >= 0 && SDR_ABL(a.ablate) != 1)
       stage_load<D, T, R, DEMOD, NW, NCH, SRC>(tile_ref<D, T, R, DEMOD, NW, NCH, SRC>(a, next), n, tid, v0, v1);
 
     // ---- 2. slide down this lane's window, R outputs x NCH channels in registers
@@ -879,7 +879,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
       acc0[r] = 0.0f;
       acc1[r] = 0.0f;
     }
-    if (a.ablate == 2) {
+    if (SDR_ABL(a.ablate) == 2) {
       acc0[0] = lds0[lbase];
       acc1[0] = lds1[lbase];
     } else {
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
           constexpr int k0 = decltype(pi)::value * KP;
           constexpr int k1 = k0 + KP < T ? k0 + KP : T;
           // ablate 4 (timing only): one pass of three -- how much a cheaper scan buys
-          if (a.ablate == 4 && k0 > 0) return;
+          if (SDR_ABL(a.ablate) == 4 && k0 > 0) return;
 #pragma unroll
           for (int i = 0; i < k1 - k0; ++i) hs[i] = hc[k0 + i];
 #pragma unroll
@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   Stage v;
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.ablate != 1) stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
+  if (SDR_ABL(a.ablate) != 1) stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
   if constexpr (SRC == Src::F32) {
     stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds, lds, lane, v, v);
   } else {
@@ -1219,7 +1219,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   wave_sync();  // a wave reads only its own slice
   const int lbase = D * R * lane;
   float acc[R];
-  if (a.ablate == 2) {
+  if (SDR_ABL(a.ablate) == 2) {
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = lds[lbase + r];
   } else {
@@ -1393,22 +1393,22 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   const long long total = (long long)a.tiles_per_stream * a.nstreams;
   if (total <= 0 || total > 0x7fffffffLL) return hipErrorInvalidValue;
   const long long ncu = device_cu_count();
-  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
+  static const int ablate = SDR_TIMING_ENV("SDR_ABLATE", 0);  // timing builds only
   a.ablate = ablate;
-  static const int persist_env = env_int("SDR_FIR_PERSIST", -1);  // A/B
+  static const int persist_env = SDR_TIMING_ENV("SDR_FIR_PERSIST", -1);  // A/B, timing builds
   if (persist_env >= 0) persist = persist_env != 0;
   if (persist) {
     // a CU's LDS (160 KiB on gfx950, read from the device), less the claim counter
     const long long kLds = (long long)device_lds_bytes() - 64;
     constexpr long long slice = (long long)G::SMEM * sizeof(float);
     if (kLds < slice) return hipErrorInvalidConfiguration;
-    static const int wpg_env = env_int("SDR_FIR_WPG", 0);  // timing experiments
+    static const int wpg_env = SDR_TIMING_ENV("SDR_FIR_WPG", 0);  // timing builds
     long long wpg = std::min<long long>(16, kLds / slice);
     if (wpg_env > 0) wpg = std::min<long long>(wpg, wpg_env);
     const long long wg_per_cu = std::max<long long>(1, std::min<long long>(32 / wpg, kLds / (wpg * slice)));
     long long groups = std::min<long long>(ncu * wg_per_cu, (total + wpg - 1) / wpg);
     // timing experiments: about k tiles per wave, as many groups as that takes
-    static const int wave_tiles = env_int("SDR_FIR_WAVE_TILES", 0);
+    static const int wave_tiles = SDR_TIMING_ENV("SDR_FIR_WAVE_TILES", 0);
     if (wave_tiles > 0) groups = std::max<long long>(8, (total + wpg * wave_tiles - 1) / (wpg * wave_tiles) + 7);
     if (total >= 64 && groups >= 8) {
       groups -= groups % 8;
@@ -1424,7 +1424,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
                        dim3((unsigned)(64 * wpg)), (size_t)(wpg * slice), st, a, h);
     return hipGetLastError();
   }
-  static const int per_cu_env = env_int("SDR_WG_PER_CU", 0);
+  static const int per_cu_env = SDR_TIMING_ENV("SDR_WG_PER_CU", 0);
   const int per_cu = per_cu_env > 0 ? per_cu_env : wpc;
   const long long slots = ncu * per_cu * 4 / NW;  // ~per_cu waves per CU
   long long blocks;
@@ -1456,7 +1456,7 @@ hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
   a.tiles_per_stream = nout > G::E ? (int)((nout - G::E + G::ADV - 1) / G::ADV) : 1;
   const long long total = (long long)a.tiles_per_stream * a.nstreams;
   if (total <= 0 || total > 0x7fffffffLL - 8) return hipErrorInvalidValue;
-  static const int ablate = env_int("SDR_ABLATE", 0);  // timing experiments only
+  static const int ablate = SDR_TIMING_ENV("SDR_ABLATE", 0);  // timing builds only
   a.ablate = ablate;
   const long long per_xcd = (total + 7) / 8;
   const size_t lds = (size_t)(2 * G::LDS_LEN + 64 * R) * sizeof(float);
@@ -1466,18 +1466,12 @@ hipError_t run_tile_sc(const FirLaunch& a0, const float* h, hipStream_t st) {
 
 // The fused f32 front end runs fir_tile_sc (same box: 0.0978-0.0990 vs
 // 0.1015-0.1056 ms on cfg2, profiles/r03_ab/cfg2_split_channel.txt);
-// SDR_FIR_SC=0 selects fir_tile (read per launch, so a test runs both)
-bool sc_enabled() {
-  const char* e = std::getenv("SDR_FIR_SC");
-  return !e || std::atoi(e) != 0;
-}
+// switch SDR_FIR_SC=0 selects fir_tile (the tests run both)
+bool sc_enabled() { return sw(kSwFirSc) != 0; }
 // the u8 wire path on fir_tile_sc too (cfg2u8 0.0806-0.0813 -> 0.0785-0.0788
 // ms, mono0 -1 % on one box); SDR_FIR_SC_U8=0 selects the persistent
-// fir_tile_grp (read per launch, so a test runs both)
-bool sc_u8_enabled() {
-  const char* e = std::getenv("SDR_FIR_SC_U8");
-  return !e || std::atoi(e) != 0;
-}
+// fir_tile_grp (switch SDR_FIR_SC_U8; the tests run both)
+bool sc_u8_enabled() { return sw(kSwFirScU8) != 0; }
 
 // Tile shape per decimation factor: R outputs per lane, one wave per
 // workgroup, taps in SGPRs (TM 1), waves per CU.  D*R must

@@ -236,7 +236,7 @@ __global__ __launch_bounds__(1024, 1) void resample_pp(PPArgs a) {
   }
 
   auto compute = [&](long long cb, const float* img) __attribute__((always_inline)) {
-    if (!wave_on || a.ablate == 2) return;
+    if (!wave_on || SDR_ABL(a.ablate) == 2) return;
     const long long col = cb * kPPLanes + ln;
     const long long sidx = col / a.np, t = col - sidx * a.np;
     const long long j = (long long)a.up * t + phi;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(1024, 1) void resample_pp(PPArgs a) {
     if (col < a.ncols && j < a.ny) a.y[sidx * a.y_stride + j] = acc;
   };
   auto stage = [&](long long cb, float* img, bool edge) __attribute__((always_inline)) {
-    if (a.ablate == 1) return;
+    if (SDR_ABL(a.ablate) == 1) return;
     if (edge)
       pp_edge<CMAX>(a, cb, img, wv, ln, nw, q0, sa, per_col);
     else
@@ -314,11 +314,8 @@ __global__ __launch_bounds__(kWG) void resample_commit(const float* __restrict__
   state[(long long)s * ns + i] = x[(long long)s * x_stride + n - ns + i];
 }
 
-// read per launch (a getenv scan), so a test can switch kernels in-process
-bool pp_enabled() {
-  const char* e = std::getenv("SDR_RESAMPLE_PP");
-  return !e || std::atoi(e) != 0;
-}
+// switch SDR_RESAMPLE_PP (the tests run every resampler kernel)
+bool pp_enabled() { return sw(kSwResamplePp) != 0; }
 
 }  // namespace
 
@@ -375,7 +372,7 @@ hipError_t launch_resample(int up, int down, const float* x, long long n, int ns
     if ((segpad / 4) % 2 == 0) segpad += 4;
     a.segpad = segpad;
     a.vec = (down % 4 == 0) && x_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    static const int ablate = env_int("SDR_ABLATE", 0);
+    static const int ablate = SDR_TIMING_ENV("SDR_ABLATE", 0);
     a.ablate = ablate;
     const long long seglen_max = qspan + cnt_max + 3;  // one DMA wave-instruction per column
     if (segpad <= kPPSeg && seglen_max <= 256 && a.vec) {

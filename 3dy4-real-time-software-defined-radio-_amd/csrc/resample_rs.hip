@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64 * kRsWaves, 1) void resample_rs(RsArgs a) {
     // a new column block: the first group's whole window
     int lo, hi;
     need(0, lo, hi);
-    if (a.ablate != 1) {
+    if (SDR_ABL(a.ablate) != 1) {
       rs_dma<CMAX>(a, ring, cb, wv, ln, base0, lo, hi);
       rs_edge<CMAX>(a, ring, cb, wv, ln, base0, lo, hi);
     }
@@ -234,12 +234,12 @@ __global__ __launch_bounds__(64 * kRsWaves, 1) void resample_rs(RsArgs a) {
       if (more) {
         need(g + 1, nlo, nhi);
         nlo = have;
-        if (a.ablate != 1 && nhi > nlo) rs_dma<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
+        if (SDR_ABL(a.ablate) != 1 && nhi > nlo) rs_dma<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
         fetch_taps(g + 1, tv);  // registers; written to LDS after this group is done
       }
       // this wave's two phases
       const int pa = g * kRsPG + wv, pb = pa + kRsWaves;
-      if (pa < a.up && a.ablate != 2) {
+      if (pa < a.up && SDR_ABL(a.ablate) != 2) {
         const bool on1 = pb < a.up;
         const int pbb = on1 ? pb : pa;
         const int qa = pa * a.down / a.up, qb = pbb * a.down / a.up;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64 * kRsWaves, 1) void resample_rs(RsArgs a) {
           if (on1 && jb < a.ny) ys[jb] = acc1;
         }
       }
-      if (more && a.ablate != 1 && nhi > nlo) rs_edge<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
+      if (more && SDR_ABL(a.ablate) != 1 && nhi > nlo) rs_edge<CMAX>(a, ring, cb, wv, ln, base0, nlo, nhi);
       if (more) have = nhi > have ? nhi : have;
       dma_drain();
       __syncthreads();  // the next group's chunks have landed; this group's reads are done
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   const int i1 = i0 + per + ((int)blockIdx.x < extra ? 1 : 0);
   if (i0 >= i1) return;
   auto stage = [&](float* buf, int it) __attribute__((always_inline)) {
-    if (a.ablate == 1) return;
+    if (SDR_ABL(a.ablate) == 1) return;
     if (!LW)
       lp_stage<CMAX>(a, buf, it, threadIdx.x, kLpSlots, wv, kLpWaves, ln);
     else if (loader)
@@ -607,7 +607,7 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   for (int it = i0; it < i1; ++it) {
     // (the previous item drained its DMAs before its output stores; the
     // loader drains its own here)
-    if (it == i0 || a.ablate == 2 || loader) dma_drain();
+    if (it == i0 || SDR_ABL(a.ablate) == 2 || loader) dma_drain();
     __syncthreads();  // item it's span has landed; the other buffer is free
     // the stream's first item is the only reader of its old state and its span
     // is staged now: state <- last ns inputs of the block (src/filter.cpp:169)
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
                                        cbuf + wv * 64, 4, 0, 0);
     }
     if (!(SDR_LP_EARLY && LW) && it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
-    if (a.ablate != 2 && !loader) {
+    if (SDR_ABL(a.ablate) != 2 && !loader) {
       if (odd)
         lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
       else
@@ -642,23 +642,10 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   }
 }
 
-// read per launch (a getenv scan), so a test can switch kernels in-process
-bool lp_enabled() {
-  const char* e = std::getenv("SDR_RESAMPLE_LP");
-  return !e || std::atoi(e) != 0;
-}
-
-// read per launch (a getenv scan), so a test can switch kernels in-process
-bool lp_loader() {
-  const char* e = std::getenv("SDR_RESAMPLE_LOADER");
-  return !e || std::atoi(e) != 0;
-}
-
-// read per launch (a getenv scan), so a test can switch kernels in-process
-bool rs_enabled() {
-  const char* e = std::getenv("SDR_RESAMPLE_RS");
-  return !e || std::atoi(e) != 0;
-}
+// switches SDR_RESAMPLE_LP / _LOADER / _RS (the tests run every resampler kernel)
+bool lp_enabled() { return sw(kSwResampleLp) != 0; }
+bool lp_loader() { return sw(kSwResampleLoader) != 0; }
+bool rs_enabled() { return sw(kSwResampleRs) != 0; }
 
 }  // namespace
 
@@ -722,7 +709,7 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
   const long long span = ((long long)(kRsPG - 1) * down + up - 1) / up + cmax + 8;
   const long long step = ((long long)kRsPG * down + up - 1) / up + 8;
   if (!use_lp && (!rs_enabled() || span + step > kRsRing)) return false;
-  static const int ablate = env_int("SDR_ABLATE", 0);
+  static const int ablate = SDR_TIMING_ENV("SDR_ABLATE", 0);
   const int ncu = device_cu_count();
   if (use_lp) {
     const int S = lpS, K = lpK, C = lpC;
@@ -757,11 +744,14 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
       }
       const int grid = b.nitems < ncu ? b.nitems : ncu;
       const dim3 g((unsigned)grid);
+#ifdef SDR_TIMING_BUILD
       if (ablate == 4 && cmax == 151 && K == 7) {
         // timing ablation: no staging and no LDS reads in the scan
         b.ablate = 1;
         hipLaunchKernelGGL((resample_lp<151, 7, 1, 1>), g, dim3(kLpSlots + 64), 0, st, b);
-      } else if (lp_loader()) {
+      } else
+#endif
+      if (lp_loader()) {
         const dim3 blk(kLpSlots + 64);
         if (cmax == 151) {
           if (K == 4)

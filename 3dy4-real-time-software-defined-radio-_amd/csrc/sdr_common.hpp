@@ -44,7 +44,7 @@ struct FirLaunch {
   int tiles_per_wg;  // fir_tile: tiles per workgroup (see fir_tile.hip)
   int walk;          // fir_tile: 0 a run per workgroup, 1 XCD slabs; fir_tile_grp: 1 XCD slabs, 0 one slab
   int slab;          // fir_tile_grp: tiles per slab
-  int ablate;        // timing experiments only (SDR_ABLATE): 1 = no global loads, 2 = no FIR math, 4 = one tap pass of three
+  int ablate;        // timing builds only (SDR_ABL): 1 = no global loads, 2 = no FIR math, 4 = one tap pass of three
   int fma;           // SDR_ARITH_FMA: fused multiply-add FIR arithmetic where a fast path implements it
 };
 
@@ -67,8 +67,45 @@ __device__ __forceinline__ float u8_byte_to_f32(uint32_t w) {
 int device_cu_count();
 int device_lds_bytes();  // LDS bytes per CU of the current device
 int device_grid_y_max();  // grid y limit of the current device (kernels put streams on y)
-// Integer environment switch (timing experiments), `dflt` when unset.
+// Integer environment variable, `dflt` when unset.  Read at context creation
+// (SDR_STEREO_FORK) and, once, by the switch table below -- never per launch.
 int env_int(const char* name, int dflt);
+
+// Kernel-selection switches: which of several bit-identical kernels a
+// launcher runs (A/B and the parity tests, which run every kernel).  One
+// process-wide table of atomics, initialised once from the environment
+// variable of the same name (first use), then changed only through
+// sdr_set_switch() (include/sdr_hip.h).  Launchers read it with one relaxed
+// atomic load: no environment scan in the launch path, and no getenv racing a
+// setenv in a multithreaded caller.
+enum Switch : int {
+  kSwFirSc = 0,       // SDR_FIR_SC: f32 fused front end on fir_tile_sc (1) or fir_tile (0)
+  kSwFirScU8,         // SDR_FIR_SC_U8: u8 front end on fir_tile_sc (1) or persistent fir_tile_grp (0)
+  kSwResampleLp,      // SDR_RESAMPLE_LP: lane-phase resample_lp for the shapes it covers
+  kSwResampleLoader,  // SDR_RESAMPLE_LOADER: resample_lp with its loader wave
+  kSwResampleRs,      // SDR_RESAMPLE_RS: sliding-window resample_rs
+  kSwResamplePp,      // SDR_RESAMPLE_PP: phase-major resample_pp
+  kSwLongVtap,        // SDR_LONG_VTAP: fir_long with LDS-staged (1) or SGPR (0) taps
+  kSwF16Mfma,         // SDR_F16_MFMA: fp16 arm on the MFMA Toeplitz GEMM (1) or v_dot2 (0)
+  kSwF16Head,         // SDR_F16_HEAD: fir_long_mfma's first workgroup loads its state in the first batch
+  kSwF16W8,           // SDR_F16_W8: fir_long_mfma as 8 waves of one tile (1) or 4 of two (0)
+  kSwPllFast,         // SDR_PLL_FAST: certified short-chain PLL step (1) or library routines (0)
+  kSwPllGuard,        // SDR_PLL_GUARD: the PLL's chunk input checks as a parallel pre-pass
+  kSwCount
+};
+int sw(Switch s);
+
+// Timing experiments (ablations that return WRONG outputs, shape overrides)
+// exist only in a timing build (make TIMING=1 -> -DSDR_TIMING_BUILD, never
+// the shipped library): in the product build the ablation field is the
+// constant 0 and the variables are not even named.
+#ifdef SDR_TIMING_BUILD
+#define SDR_TIMING_ENV(name, dflt) (::sdr::env_int((name), (dflt)))
+#define SDR_ABL(v) (v)
+#else
+#define SDR_TIMING_ENV(name, dflt) (dflt)
+#define SDR_ABL(v) 0
+#endif
 
 // Host-side launchers, one per kernel family (defined next to the kernels).
 // allow_fast = false forces the generic kernel (misaligned buffers).

@@ -260,20 +260,23 @@ hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, lon
   const long long nchunk = n / kPllChunk;
   // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests);
   // SDR_PLL_GUARD=0 evaluates the input check inside the recurrence (A/B)
-  const int fast = env_int("SDR_PLL_FAST", 1);
+  const int fast = sw(kSwPllFast);  // (mode 2, no re-run path, exists in timing builds only)
   // (the pre-pass puts the streams on grid y: past the device's grid-y limit
   // the recurrence evaluates the guard itself -- same bits)
-  const bool pre = guard && nchunk > 0 && env_int("SDR_PLL_GUARD", 1) != 0 && nstreams <= device_grid_y_max();
+  const bool pre = guard && nchunk > 0 && sw(kSwPllGuard) != 0 && nstreams <= device_grid_y_max();
   if (fast && pre) {
     hipLaunchKernelGGL(pll_guard_kernel, dim3((unsigned)((nchunk + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0,
                        st, in, nstreams, in_stride, guard, nchunk);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+#ifdef SDR_TIMING_BUILD
   if (fast == 2)
     hipLaunchKernelGGL((pll_kernel<2, 0>), grid, block, 0, st, in, n, nstreams, in_stride, freq, Fs, nco_scale,
                        phase_adjust, norm_bw, pll, args, args_stride, nullptr, 0LL);
-  else if (fast && pre)
+  else
+#endif
+  if (fast && pre)
     hipLaunchKernelGGL((pll_kernel<1, 1>), grid, block, 0, st, in, n, nstreams, in_stride, freq, Fs, nco_scale,
                        phase_adjust, norm_bw, pll, args, args_stride, guard, nchunk);
   else if (fast)

@@ -48,6 +48,8 @@ _SIGS = {
     "sdr_version": [],
     "sdr_strerror": [_i],
     "sdr_device_count": [C.POINTER(_i)],
+    "sdr_set_switch": [C.c_char_p, _i],
+    "sdr_get_switch": [C.c_char_p, C.POINTER(_i)],
     "sdr_ctx_create": [_i, C.POINTER(_vp)],
     "sdr_ctx_destroy": [_vp],
     "sdr_ctx_set_stream": [_vp, _vp],
@@ -108,8 +110,6 @@ _SIGS = {
     "sdr_stereo_work_destroy": [_vp, _vp],
     "sdr_stereo_front_u8_dev": [_vp, _vp, _ll, _vp, _vp, _vp],
     "sdr_stereo_back_dev": [_vp, C.c_float, _vp, _vp, _vp, _vp, _ll],
-    "sdr_stereo_pll_dev": [_vp, C.c_float, _vp, _vp],
-    "sdr_stereo_post_dev": [_vp, _vp, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
 }
@@ -155,6 +155,43 @@ def lib() -> C.CDLL:
 
 def version() -> str:
     return lib().sdr_version().decode()
+
+
+SWITCHES = ("SDR_FIR_SC", "SDR_FIR_SC_U8", "SDR_RESAMPLE_LP", "SDR_RESAMPLE_LOADER", "SDR_RESAMPLE_RS",
+            "SDR_RESAMPLE_PP", "SDR_LONG_VTAP", "SDR_F16_MFMA", "SDR_F16_HEAD", "SDR_F16_W8", "SDR_PLL_FAST",
+            "SDR_PLL_GUARD")
+
+
+def set_switch(name: str, value: int) -> None:
+    """sdr_set_switch: pick one of several bit-identical kernels, process-wide
+    (include/sdr_hip.h); applies to launches enqueued after the call."""
+    if lib().sdr_set_switch(name.encode(), int(value)) != SDR_OK:
+        raise ValueError(f"unknown kernel switch {name!r}")
+
+
+def get_switch(name: str) -> int:
+    v = _i(0)
+    if lib().sdr_get_switch(name.encode(), C.byref(v)) != SDR_OK:
+        raise ValueError(f"unknown kernel switch {name!r}")
+    return v.value
+
+
+class switches:
+    """Context manager: set kernel switches for a block, restore them after."""
+
+    def __init__(self, **values):
+        self._new = {k: int(v) for k, v in values.items()}
+        self._old = {}
+
+    def __enter__(self):
+        for k, v in self._new.items():
+            self._old[k] = get_switch(k)
+            set_switch(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self._old.items():
+            set_switch(k, v)
 
 
 def device_count() -> int:
@@ -497,15 +534,6 @@ class Context:
         """Front stage of the stereo path (src/project.cpp:72-121) into `work`."""
         self._check(lib().sdr_stereo_front_u8_dev(self._c, _ptr(iq), iq_stride, C.addressof(taps),
                                                   C.addressof(state), work._w), "stereo_front_u8_dev")
-
-    def stereo_pll_dev(self, audio_fs, state, work):
-        """sdr_stereo_pll_dev: the back stage's PLL recurrence only."""
-        self._check(lib().sdr_stereo_pll_dev(self._c, audio_fs, C.addressof(state), work._w), "stereo_pll_dev")
-
-    def stereo_post_dev(self, taps, state, work, pcm, pcm_stride):
-        """sdr_stereo_post_dev: NCO x stereo band, stereo resampler, L/R s16."""
-        self._check(lib().sdr_stereo_post_dev(self._c, C.addressof(taps), C.addressof(state), work._w, _ptr(pcm),
-                                              pcm_stride), "stereo_post_dev")
 
     def stereo_back_dev(self, audio_fs, taps, state, work, pcm, pcm_stride):
         """Back stage (PLL recurrence onwards, :123-132 + 304-314) from `work` to s16 L/R."""

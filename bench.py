@@ -108,10 +108,11 @@ def parse(argv=None):
     ap.add_argument("--batches", type=int, default=2, help="distinct input batches the steps cycle over")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per replayed HIP graph")
     ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
-    ap.add_argument("--stereo-pipeline", type=int, default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "1")),
+    ap.add_argument("--stereo-pipeline", type=int, choices=(0, 1),
+                    default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "1")),
                     help="stereo configs: 1 = each step as two stages on two contexts' streams (front end + band-pass "
-                         "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence; 2 = "
-                         "three stages on three contexts (front | recurrence | NCO, stereo resampler, PCM)")
+                         "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence; 0 = "
+                         "one call per step")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
                     help="after the timed window, time this many seconds of back-to-back steps (the "
                          "`sustained` field: a receiver runs the block loop continuously); 0 skips it")
@@ -326,21 +327,11 @@ class Job:
                 ctx2 = self.ctx2 = sdrhip.Context(device)
                 self.stream2 = torch.cuda.Stream(dev)
                 ctx2.set_stream(self.stream2.cuda_stream)
-                three = args.stereo_pipeline == 2
-                ctx3 = None
-                if three:
-                    # step b's post stage (NCO, stereo resampler, PCM) on a third
-                    # context, beside step b+1's recurrence: the recurrence needs
-                    # only the previous step's PLL state
-                    ctx3 = self.ctx3 = sdrhip.Context(device)
-                    self.stream3 = torch.cuda.Stream(dev)
-                    ctx3.set_stream(self.stream3.cuda_stream)
-                nslot = 3 if three else 2
+                nslot = 2
                 works = [ctx.stereo_work(D, n, up, down, S) for _ in range(nslot)]
                 ev_f = [sdrhip.Event(ctx) for _ in range(nslot)]
-                ev_p = [sdrhip.Event(ctx) for _ in range(nslot)]
                 ev_b = [sdrhip.Event(ctx) for _ in range(nslot)]
-                self.keep += [works, ev_f, ev_p, ev_b]
+                self.keep += [works, ev_f, ev_b]
 
                 def seq(j0, k):
                     """k consecutive steps; the first nslot wait on nothing (whatever ran
@@ -353,15 +344,8 @@ class Job:
                         ctx.stereo_front_u8_dev(iqs[(j0 + j) % len(iqs)], 2 * n, taps_s, state_s, works[slot])
                         ev_f[slot].record(ctx)
                         ev_f[slot].wait(ctx2)
-                        if three:
-                            ctx2.stereo_pll_dev(240e3, state_s, works[slot])
-                            ev_p[slot].record(ctx2)
-                            ev_p[slot].wait(ctx3)
-                            ctx3.stereo_post_dev(taps_s, state_s, works[slot], pcm, 2 * na)
-                            ev_b[slot].record(ctx3)
-                        else:
-                            ctx2.stereo_back_dev(240e3, taps_s, state_s, works[slot], pcm, 2 * na)
-                            ev_b[slot].record(ctx2)
+                        ctx2.stereo_back_dev(240e3, taps_s, state_s, works[slot], pcm, 2 * na)
+                        ev_b[slot].record(ctx2)
                     if k:
                         ev_b[(j0 + k - 1) % nslot].wait(ctx)
                 self.seq = seq
@@ -478,9 +462,8 @@ class Job:
         self._next = (self._next + k) % len(self.steps)
 
     _next = 0
-    seq = None  # a step sequencer (two- or three-stage stereo pipeline) instead of one call per step
+    seq = None  # a step sequencer (two-stage stereo pipeline) instead of one call per step
     ctx2 = None
-    ctx3 = None
 
     def capture(self, gs: int):
         """Record gs consecutive steps into a HIP graph (gs a multiple of the batch
@@ -492,10 +475,8 @@ class Job:
         self._next = 0
         if self.seq is not None:
             self.graph = (self.ctx.capture(lambda: self.seq(0, gs)), gs)
-            # the other stages' contexts: their scratch must not grow under the graph
+            # the back stage's context: its scratch must not grow under the graph
             self.ctx2.pin_scratch(True)
-            if self.ctx3 is not None:
-                self.ctx3.pin_scratch(True)
         else:
             self.graph = (self.ctx.capture(lambda: [self.steps[j % nb]() for j in range(gs)]), gs)
 
@@ -550,8 +531,6 @@ class Job:
                     obj.close()
         if self.ctx2 is not None:
             self.ctx2.close()
-        if self.ctx3 is not None:
-            self.ctx3.close()
         self.ctx.close()
 
 
@@ -735,10 +714,7 @@ def main(argv=None):
                                       f"({'one host thread per device' if plan['mode'] == 'threads' else 'one process per device, gloo timing barrier'})",
                        "devices_opened": distinct, "input_batches": max(1, args.batches),
                        "launch": "direct" if args.no_graph else f"HIP graph of {args.graph_steps} steps",
-                       **({"stereo_pipeline": ("three stages on three contexts' streams (front | PLL recurrence | "
-                                               "NCO, stereo resampler, PCM), steps overlapping stage by stage"
-                                               if args.stereo_pipeline == 2 else
-                                               "two stages on two contexts' streams (front | PLL onwards), step "
+                       **({"stereo_pipeline": ("two stages on two contexts' streams (front | PLL onwards), step "
                                                "b+1's front overlapping step b's recurrence")
                            if args.stereo_pipeline else "one call per step"} if job["kind"] == "stereo_u8" else {}),
                        "state_carried_across_steps": True,

@@ -89,6 +89,20 @@ int sdr_ctx_set_arith(sdr_ctx *ctx, int mode);
 #define SDR_FORK_SIDE 1
 int sdr_ctx_set_stereo_fork(sdr_ctx *ctx, int mode);
 
+/* Kernel-selection switches (process-wide).  Several calls have more than
+ * one kernel with identical outputs (bit-identical, or -- fp16 arm -- the same
+ * tolerance contract); a switch picks one, for A/B timing and for the parity
+ * tests, which run every kernel.  Each switch starts at the environment
+ * variable of the same name if it is set when the library first needs it,
+ * else at the measured default, and is then changed only by
+ * sdr_set_switch: launches read it without scanning the environment.  Names:
+ * SDR_FIR_SC, SDR_FIR_SC_U8, SDR_RESAMPLE_LP, SDR_RESAMPLE_LOADER,
+ * SDR_RESAMPLE_RS, SDR_RESAMPLE_PP, SDR_LONG_VTAP, SDR_F16_MFMA,
+ * SDR_F16_HEAD, SDR_F16_W8, SDR_PLL_FAST, SDR_PLL_GUARD.  An unknown name is
+ * SDR_EINVAL.  A change applies to launches enqueued after it. */
+int sdr_set_switch(const char *name, int value);
+int sdr_get_switch(const char *name, int *value);
+
 /* Device memory helpers so a C/C++ caller needs no HIP headers. */
 int sdr_dev_alloc(sdr_ctx *ctx, size_t bytes, void **ptr);
 int sdr_dev_free(sdr_ctx *ctx, void *ptr);
@@ -206,9 +220,10 @@ int sdr_resample_f32_dev(sdr_ctx *ctx, int up, int down, const float *x, long lo
  * single launch.  h is read at creation by that kernel and at each call by
  * the fallback kernels (other shapes): it must not change while the plan
  * lives.  Same outputs, state and preconditions as sdr_resample_f32_dev.
- * sdr_resample_plan_destroy waits for the last direct call on every stream
- * that used the plan (one event per stream), not for the whole device; graphs
- * that recorded calls with the plan must be destroyed before it. */
+ * sdr_resample_plan_destroy waits for the table build and for the last
+ * direct call on every stream that used the plan (one event per stream), not
+ * for the whole device; graph replays of calls with the plan must have
+ * completed (not only been destroyed) before it. */
 typedef struct sdr_resample_plan sdr_resample_plan;
 int sdr_resample_plan_create(sdr_ctx *ctx, int up, int down, const float *h, int ntaps,
                              sdr_resample_plan **plan);
@@ -315,6 +330,9 @@ int sdr_stereo_pcm_u8_dev(sdr_ctx *ctx, int D, const uint8_t *iq, long long npai
  * back stage runs on another's -- order them with sdr_event_record /
  * sdr_ctx_wait_event and give each block in flight its own work object
  * (host/sdr_project.cpp).  Outputs equal sdr_stereo_pcm_u8_dev's. */
+/* sdr_stereo_work_destroy waits for every direct front / back call on every
+ * context's stream that used the work (one event per stream), then frees it;
+ * graph replays of calls with the work must have completed before it. */
 typedef struct sdr_stereo_work sdr_stereo_work;
 int sdr_stereo_work_create(sdr_ctx *ctx, int D, long long npairs, int up, int down, int nstreams,
                            sdr_stereo_work **work);
@@ -323,15 +341,6 @@ int sdr_stereo_front_u8_dev(sdr_ctx *ctx, const uint8_t *iq, long long iq_stride
                             sdr_stereo_state *state, sdr_stereo_work *work);
 int sdr_stereo_back_dev(sdr_ctx *ctx, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
                         sdr_stereo_work *work, int16_t *pcm, long long pcm_stride);
-/* sdr_stereo_back_dev as two stages (a three-stage pipeline: block b+1's
- * recurrence needs block b's PLL state only, not its post stage):
- * sdr_stereo_pll_dev the recurrence (src/project.cpp:123-126, state->pll),
- * sdr_stereo_post_dev NCO x stereo band, stereo resampler, L/R s16
- * (:127-132, 304-314; state->stereo_lp_state).  Each stage's state is its
- * own, so each may run on its own context's stream, ordered by events. */
-int sdr_stereo_pll_dev(sdr_ctx *ctx, float audio_fs, sdr_stereo_state *state, sdr_stereo_work *work);
-int sdr_stereo_post_dev(sdr_ctx *ctx, const sdr_stereo_taps *taps, sdr_stereo_state *state, sdr_stereo_work *work,
-                        int16_t *pcm, long long pcm_stride);
 
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the

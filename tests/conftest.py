@@ -50,6 +50,22 @@ def built_lib():
     return sdrhip
 
 
+@pytest.fixture
+def kswitch(built_lib):
+    """kswitch(name, value): pick a kernel through sdr_set_switch (process-wide,
+    include/sdr_hip.h) for one test; every switch it touched is restored after."""
+    old = {}
+
+    def set_(name, value):
+        if name not in old:
+            old[name] = built_lib.get_switch(name)
+        built_lib.set_switch(name, int(value))
+
+    yield set_
+    for k, v in old.items():
+        built_lib.set_switch(k, v)
+
+
 @pytest.fixture(scope="session")
 def manifest():
     with open(os.path.join(GOLDEN, "MANIFEST.json")) as f:
@@ -101,3 +117,17 @@ def assert_bits(a, b, what=""):
         i = bad[0]
         raise AssertionError(f"{what}: {len(bad)} of {a.size} elements differ in bits; first at {i}: "
                              f"{a.flat[i]!r} vs {b.flat[i]!r}; max |diff| {np.nanmax(np.abs(a - b)):.3g}")
+
+
+def assert_bits_nan(a, b, what=""):
+    """Bitwise where `b` (the reference) is a number or an infinity, NaN exactly
+    where it is NaN (payloads may differ: x86 and gfx950 quiet NaNs differ)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    assert a.shape == b.shape, f"{what}: shape {a.shape} != {b.shape}"
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        bad = np.flatnonzero(na != nb)
+        raise AssertionError(f"{what}: NaN positions differ at {len(bad)} of {a.size} elements; first at {bad[0]}: "
+                             f"{a.flat[bad[0]]!r} vs {b.flat[bad[0]]!r}")
+    assert_bits(a[~nb], b[~nb], what)

@@ -176,11 +176,123 @@ def main():
          inter=ref.interleave(x[:100], y[:100]), conv=ref.convolve_full(x[:300], taps["pilot_mode0"]),
          down=ref.downsample(x[:303], 10), up=ref.upsample(x[:40], 3))
 
+    nonfinite_cases(ref, taps)
+    write_manifest()
+
+
+def write_manifest():
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     total = sum(os.path.getsize(os.path.join(HERE, n + ".npz")) for n in manifest["cases"])
     print(f"wrote {len(manifest['cases'])} fixtures, {total / 1024:.0f} KiB")
 
 
+def nonfinite_cases(ref, taps):
+    """Inf / -Inf / NaN in the samples and in the carried state, and sums that
+    overflow to Inf (Inf envelopes in the discriminator, Inf - Inf = NaN): the
+    reference propagates them term by term (src/filter.cpp:66-140) and its
+    `param == 0` rule (:89-92) meets them.  Several independent streams, each
+    with its own pattern, two blocks each (the state carries them on)."""
+    from sdrhip.synth import fm_planar
+
+    inf, nan = np.float32(np.inf), np.float32(np.nan)
+
+    def streams(nstreams, n, seed):
+        I = np.empty((nstreams, n), np.float32)
+        Q = np.empty((nstreams, n), np.float32)
+        for s in range(nstreams):
+            I[s], Q[s] = fm_planar(n, seed=seed + s)
+        return I, Q
+
+    # ---- fused front end, D = 10, blocks of 5,130 pairs (n % 4 = 2: a chunk straddles the block end)
+    D, block, nblk, S, ns = 10, 5130, 2, 7, 100
+    n = block * nblk
+    I, Q = streams(S, n, SEED + 40)
+    si0 = np.random.default_rng(SEED + 41).uniform(-0.5, 0.5, (S, ns)).astype(np.float32)
+    sq0 = np.random.default_rng(SEED + 42).uniform(-0.5, 0.5, (S, ns)).astype(np.float32)
+    prev0 = np.zeros((S, 2), np.float32)
+    I[0, 0], I[0, 2600] = nan, inf                       # a stream's first sample; mid-block
+    Q[1, 3], Q[1, block - 1] = -inf, nan                 # near the start; the block's last (-> carried state)
+    si0[2, 50], sq0[2, 99], prev0[2, 0] = inf, nan, nan  # carried state and prev_I
+    I[3, n - 2], Q[3, n - 3] = -inf, inf                 # the last 3 samples of the final block
+    I[4, 1000:1040], Q[4, 1000:1040] = 3e38, -3e38       # finite inputs, sums overflow to +-Inf
+    I[5, 3000], Q[5, 3000] = inf, inf                    # Inf in both channels at once
+    I[6, block + 7], Q[6, block + 2] = nan, -inf         # second block's first tile
+    h = taps["rf_mode0"]
+    dm, st = [], []
+    for s in range(S):
+        si, sq, prev = si0[s].copy(), sq0[s].copy(), prev0[s].copy()
+        outs, sts = [], []
+        for b in range(nblk):
+            sl = slice(b * block, (b + 1) * block)
+            yi = ref.fir_decim(D, I[s, sl], h, si)
+            yq = ref.fir_decim(D, Q[s, sl], h, sq)
+            outs.append(ref.fm_demod(yi, yq, prev))
+            sts.append(np.concatenate([si, sq, prev]))
+        dm.append(np.stack(outs))
+        st.append(np.stack(sts))
+    save("nonfinite_frontend", "downsampleBlockConvolveFIR x2 + fmDemodArctan (non-finite inputs)",
+         {"D": D, "block": block, "nblk": nblk, "ntaps": len(h), "state": ns, "streams": S},
+         I=I, Q=Q, h=h, state_i0=si0, state_q0=sq0, prev0=prev0, demod=np.stack(dm), states=np.stack(st))
+
+    # ---- stateful FIR, D = 1 and D = 10 single channel: 101 taps (tiled), 1024 (long), 100 (generic)
+    def fir_case(name, D, h, ns, block, seed):
+        S, nblk = 4, 2
+        n = block * nblk
+        x, _ = streams(S, n, seed)
+        st0 = np.random.default_rng(seed + 1).uniform(-0.5, 0.5, (S, ns)).astype(np.float32)
+        x[0, 0], x[0, block // 2] = nan, inf
+        x[1, block - 1], x[1, 5] = -inf, inf            # the last sample is carried into block 2
+        st0[2, ns - 1], st0[2, ns // 3] = nan, -inf     # carried state (read by the first outputs)
+        x[3, n - 3:] = 3e38                             # the last 3 samples, sums overflow
+        ys, sts = [], []
+        for s in range(S):
+            st = st0[s].copy()
+            yy, ss = [], []
+            for b in range(nblk):
+                xb = x[s, b * block:(b + 1) * block]
+                yy.append(ref.fir_block(xb, h, st) if D == 1 else ref.fir_decim(D, xb, h, st))
+                ss.append(st.copy())
+            ys.append(np.stack(yy))
+            sts.append(np.stack(ss))
+        save(name, ("blockConvolveFIR" if D == 1 else "downsampleBlockConvolveFIR") + " (non-finite inputs)",
+             {"D": D, "ntaps": len(h), "state": ns, "block": block, "nblk": nblk, "streams": S},
+             x=x, h=h, state0=st0, y=np.stack(ys), states=np.stack(sts))
+
+    fir_case("nonfinite_fir_101", 1, taps["pilot_mode0"], 100, 5120, SEED + 50)
+    fir_case("nonfinite_fir_1024", 1, taps["cfg5_1024"], 1023, 8192, SEED + 52)
+    fir_case("nonfinite_fir_100", 1, ref.taps_lpf(240e3, 16e3, 100, 1), 99, 3000, SEED + 54)
+    fir_case("nonfinite_decim_101", 10, taps["rf_mode0"], 100, 5120, SEED + 56)
+
+    # ---- the discriminator alone: Inf and NaN in I, Q and prev, Inf envelopes
+    rng = np.random.default_rng(SEED + 60)
+    I = rng.standard_normal(300).astype(np.float32)
+    Q = rng.standard_normal(300).astype(np.float32)
+    I[[3, 10, 11, 40, 41, 90]] = [inf, -inf, inf, nan, 1.0, 3e38]
+    Q[[3, 10, 12, 40, 42, 90]] = [1.0, inf, nan, 0.0, -inf, 3e38]
+    I[[150, 151]], Q[[150, 151]] = 2e19, 2e19            # envelope overflows the float, not the double
+    I[200], Q[200] = 0.0, 0.0                            # zero envelope between non-finite neighbours
+    I[199], Q[201] = inf, nan
+    prev0 = np.array([inf, 0.5], np.float32)
+    prev = prev0.copy()
+    outs, prevs = [], []
+    segs = [(0, 100), (100, 299), (299, 300)]
+    for a, b in segs:
+        outs.append(ref.fm_demod(I[a:b], Q[a:b], prev))
+        prevs.append(prev.copy())
+    save("nonfinite_demod", "fmDemodArctan (non-finite inputs)", {"segments": segs},
+         I=I, Q=Q, prev0=prev0, out=np.concatenate(outs), prevs=np.stack(prevs))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--nonfinite"]:
+        # add the non-finite cases to an existing MANIFEST without rewriting the others
+        with open(os.path.join(HERE, "MANIFEST.json")) as f:
+            manifest.update(json.load(f))
+        ref = Reference()
+        t = {"rf_mode0": ref.taps_lpf(2.4e6, 100e3, 101, 1), "pilot_mode0": ref.taps_bpf(240e3, 18.5e3, 19.5e3, 101, 1),
+             "cfg5_1024": ref.taps_lpf(2.4e6, 100e3, 1024, 1)}
+        nonfinite_cases(ref, t)
+        write_manifest()
+    else:
+        main()

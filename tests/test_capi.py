@@ -67,6 +67,48 @@ def test_context_without_gpu_fails_loudly(built_lib):
         built_lib.Context(0)
 
 
+def test_kernel_switches(built_lib):
+    """sdr_set_switch / sdr_get_switch (include/sdr_hip.h): every documented
+    switch reads and writes, unknown names are refused, and the binding's
+    `switches` context manager restores the previous values."""
+    sdrhip = built_lib
+    for name in sdrhip.SWITCHES:
+        v = sdrhip.get_switch(name)
+        sdrhip.set_switch(name, 1 - v if v in (0, 1) else 0)
+        assert sdrhip.get_switch(name) == (1 - v if v in (0, 1) else 0)
+        sdrhip.set_switch(name, v)
+    with pytest.raises(ValueError):
+        sdrhip.set_switch("SDR_NO_SUCH_SWITCH", 1)
+    with pytest.raises(ValueError):
+        sdrhip.get_switch("SDR_ABLATE")  # a timing-build variable, not a switch
+    before = sdrhip.get_switch("SDR_FIR_SC")
+    with sdrhip.switches(SDR_FIR_SC=0, SDR_F16_W8=0):
+        assert sdrhip.get_switch("SDR_FIR_SC") == 0 and sdrhip.get_switch("SDR_F16_W8") == 0
+    assert sdrhip.get_switch("SDR_FIR_SC") == before
+    assert sdrhip.lib().sdr_set_switch(b"SDR_NOPE", 1) == sdrhip.SDR_EINVAL
+
+
+def test_switch_defaults_from_environment(built_lib):
+    """Each switch starts at the environment variable of its name when the
+    library first reads it (a fresh process), else at the measured default."""
+    code = ("import sdrhip; print(sdrhip.get_switch('SDR_FIR_SC'), sdrhip.get_switch('SDR_RESAMPLE_LOADER'), "
+            "sdrhip.get_switch('SDR_F16_MFMA'))")
+    env = dict(os.environ, SDR_FIR_SC="0", SDR_RESAMPLE_LOADER="0", PYTHONPATH=PKG)
+    env.pop("SDR_F16_MFMA", None)
+    out = subprocess.run(["python3", "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.split() == ["0", "0", "1"]
+
+
+def test_no_timing_scaffolding_in_product_library(built_lib):
+    """The shipped libsdrhip.so carries no timing ablation (those return wrong
+    outputs) and reads no environment variable per launch: the ablation and
+    shape-override variables exist only in a `make TIMING=1` build."""
+    blob = open(built_lib.LIB_PATH, "rb").read()
+    for name in (b"SDR_ABLATE", b"SDR_FIR_WPG", b"SDR_FIR_WAVE_TILES", b"SDR_WG_PER_CU", b"SDR_FIR_PERSIST"):
+        assert name not in blob, name
+    assert b"SDR_FIR_SC" in blob  # the switch table's names are there
+
+
 def test_error_strings(built_lib):
     L = built_lib.lib()
     for code in (0, -1, -2, -3, -4):

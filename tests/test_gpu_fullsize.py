@@ -7,10 +7,10 @@ benchmark times (f32 planar `frontend_dev`, state carried across steps):
   I/Q, recomputed in numpy in the reference's fp32 order) bit for bit;
 * config 2 under SDR_ARITH_FMA: every stream within the SURVEY 8(d) bar of
   the exact path;
-* config 4: 262,150-pair blocks (2 consecutive, 3 streams), and one stream
-  as a single 8,388,800-pair call (the bench's cfg4x8 per-stream call)
-  against the oracle run block by block -- block-size independence,
-  src/filter.cpp:139;
+* config 4: 262,150-pair blocks (2 consecutive, 3 streams), one stream as a
+  single 8,388,800-pair call (the bench's cfg4x8 per-stream call) and as a
+  single 67,110,400-pair call (the bench's cfg4 launch), each against the
+  oracle run block by block -- block-size independence, src/filter.cpp:139;
 * config 5: the 1024-tap FIR over 2 x 1,048,576 samples, windows at the
   start (real state), middle and end checked against the oracle (each
   window's state is the preceding 1,023 inputs, src/filter.cpp:82); its
@@ -61,9 +61,9 @@ def _planar_batch(sdrhip, ctx, nstreams, n, seed, stride=None):
 
 
 @pytest.mark.parametrize("kernel", ["tile", "sc"])
-def test_cfg2_full_f32_two_steps(gpu_ctx, oracle, built_lib, monkeypatch, kernel):
+def test_cfg2_full_f32_two_steps(gpu_ctx, oracle, built_lib, kswitch, kernel):
     """kernel: fir_tile, or fir_tile_sc (SDR_FIR_SC=1); the bench's launches either way."""
-    monkeypatch.setenv("SDR_FIR_SC", "0" if kernel == "tile" else "1")
+    kswitch("SDR_FIR_SC", "0" if kernel == "tile" else "1")
     sdrhip = built_lib
     S, n, D = 1024, 65540, 10
     nout = n // D
@@ -191,6 +191,40 @@ def test_cfg4_single_call_equals_blocks(gpu_ctx, oracle, built_lib):
     assert_bits(d_si.download(), si, "state_i")
     assert_bits(d_sq.download(), sq, "state_q")
     assert_bits(np.concatenate([d_pi.download(), d_pq.download()]), pv, "prev")
+
+
+def test_cfg4_full_single_call(gpu_ctx, oracle, built_lib):
+    """bench.py's cfg4 launch exactly: ONE stream x 67,110,400 pairs (256 x
+    262,150) in a single frontend_dev call -- about 53 k tiles of one stream
+    across the XCD-slab walk -- against the oracle run block by block over the
+    same samples (src/filter.cpp:139 block-size independence), with a
+    non-zero carried state; every output and the final state bitwise."""
+    sdrhip = built_lib
+    nblk, blk, D = 256, 262150, 10
+    n = nblk * blk
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, 1, n, 4343)
+    st0 = np.random.default_rng(7).uniform(-0.7, 0.7, (2, 100)).astype(np.float32)
+    pv0 = np.array([-0.125, 0.75], np.float32)
+    d_si, d_sq = _dev(sdrhip, gpu_ctx, st0[0]), _dev(sdrhip, gpu_ctx, st0[1])
+    d_pi, d_pq = _dev(sdrhip, gpu_ctx, pv0[:1]), _dev(sdrhip, gpu_ctx, pv0[1:])
+    d_out = sdrhip.DeviceArray(gpu_ctx, n // D * 4)
+    gpu_ctx.frontend_dev(D, d_I, d_Q, n, 1, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, n // D)
+    gpu_ctx.synchronize()
+    got = d_out.download()
+    I, Q = d_I.download(), d_Q.download()
+    d_I.free()
+    d_Q.free()
+    si, sq, pv = st0[0].copy(), st0[1].copy(), pv0.copy()
+    nb = blk // D
+    for b in range(nblk):
+        want = oracle.frontend(D, I[b * blk:(b + 1) * blk], Q[b * blk:(b + 1) * blk], h, si, sq, pv)
+        assert_bits(got[b * nb:(b + 1) * nb], want, f"one call vs oracle block {b}")
+    assert_bits(d_si.download(), si, "state_i")
+    assert_bits(d_sq.download(), sq, "state_q")
+    assert_bits(np.concatenate([d_pi.download(), d_pq.download()]), pv, "prev")
+    assert np.isfinite(got).all()
 
 
 def test_cfg5_full_windows(gpu_ctx, oracle, built_lib):

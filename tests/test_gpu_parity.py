@@ -25,9 +25,9 @@ def _blocks(a, block, nblk):
 
 @pytest.mark.parametrize("kernel", ["tile", "sc"])
 @pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
-def test_frontend_fused_golden(gpu_ctx, oracle, manifest, monkeypatch, name, kernel):
+def test_frontend_fused_golden(gpu_ctx, oracle, manifest, kswitch, name, kernel):
     """kernel: the fused f32 front end on fir_tile, or on fir_tile_sc (SDR_FIR_SC=1)."""
-    monkeypatch.setenv("SDR_FIR_SC", "0" if kernel == "tile" else "1")
+    kswitch("SDR_FIR_SC", "0" if kernel == "tile" else "1")
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     I, Q = oracle.u8_to_planar(g["iq_u8"])
@@ -40,9 +40,9 @@ def test_frontend_fused_golden(gpu_ctx, oracle, manifest, monkeypatch, name, ker
 
 @pytest.mark.parametrize("kernel", ["grp", "sc"])
 @pytest.mark.parametrize("name", ["frontend_mode0", "frontend_mode1", "frontend_block100", "frontend_65540"])
-def test_frontend_u8_golden(gpu_ctx, manifest, monkeypatch, name, kernel):
+def test_frontend_u8_golden(gpu_ctx, manifest, kswitch, name, kernel):
     """u8 wire front end on each kernel: fir_tile_grp (grp) and fir_tile_sc (sc)."""
-    monkeypatch.setenv("SDR_FIR_SC_U8", "0" if kernel == "grp" else "1")
+    kswitch("SDR_FIR_SC_U8", "0" if kernel == "grp" else "1")
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     si, sq, prev = np.zeros(100, np.float32), np.zeros(100, np.float32), np.zeros(2, np.float32)
@@ -122,15 +122,15 @@ def test_fir_decim_vs_oracle(gpu_ctx, oracle, D, ntaps, ns, n):
                                     (5, 4105, 128), (10, 110, 100), (10, 200, 180), (10, 130, 120),
                                     (10, 65530, 100), (10, 65550, 300)])
 @pytest.mark.parametrize("kernel", ["tile", "sc"])
-def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, monkeypatch, D, n, ns, kernel):
+def test_frontend_odd_shapes_vs_oracle(gpu_ctx, oracle, kswitch, D, n, ns, kernel):
     """Fused front end (f32 and u8 wire) where the tiled kernel's edge
     handling matters: n % 4 != 0 (a chunk straddles the block end), state
     lengths below and above the kernel's staged strip, blocks barely longer
     than the state (the last output's inputs reach into the old state)."""
     from sdrhip.synth import fm_iq_u8
 
-    monkeypatch.setenv("SDR_FIR_SC", "0" if kernel == "tile" else "1")
-    monkeypatch.setenv("SDR_FIR_SC_U8", "0" if kernel == "tile" else "1")
+    kswitch("SDR_FIR_SC", "0" if kernel == "tile" else "1")
+    kswitch("SDR_FIR_SC_U8", "0" if kernel == "tile" else "1")
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
     iq = fm_iq_u8(n * 3, seed=D * 100 + n + ns)
     st = {k: [np.zeros(ns, np.float32), np.zeros(ns, np.float32), np.zeros(2, np.float32)]
@@ -173,7 +173,7 @@ RESAMPLE_KERNELS = {"lpw": {"SDR_RESAMPLE_LOADER": "1"}, "lp": {"SDR_RESAMPLE_LO
 
 @pytest.mark.parametrize("kernel", list(RESAMPLE_KERNELS))
 @pytest.mark.parametrize("up,down,cnt,ns,n", RESAMPLE_CASES)
-def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
+def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, kswitch, kernel, up, down, cnt, ns, n):
     """Batched resampler (T = cnt*up) on each of its kernels -- lane-phase
     (taps in VGPRs), sliding-window and phase-major: several streams per
     launch, 16-B and dword staging (down % 4), small and large up (column
@@ -182,7 +182,7 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
     SDR_RESAMPLE_{LP,RS,PP}; shapes a kernel does not cover fall through to
     the next one, so every case is checked under every setting."""
     for k, v in RESAMPLE_KERNELS[kernel].items():
-        monkeypatch.setenv(k, v)
+        kswitch(k, v)
     sdrhip = built_lib
     nstreams = 5 if n < 10000 else 2
     rng = np.random.default_rng(up * 1000 + down)
@@ -206,13 +206,13 @@ def test_resample_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, ker
 
 @pytest.mark.parametrize("kernel", ["lpw", "lp", "rs"])
 @pytest.mark.parametrize("up,down,cnt,ns,n", [(147, 800, 151, 150, 8000), (147, 1280, 101, 100, 12800)])
-def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, monkeypatch, kernel, up, down, cnt, ns, n):
+def test_resample_nonfinite_inputs(gpu_ctx, oracle, built_lib, kswitch, kernel, up, down, cnt, ns, n):
     """Inf and NaN inputs (and in the carried state): every output equals the
     reference's -- bitwise where it is a number or an infinity, NaN where the
     reference's is NaN.  resample_lp and resample_rs pad the window ends with
     zero taps and zeroed inputs (term +0), never 0 * Inf."""
     for k, v in RESAMPLE_KERNELS[kernel].items():
-        monkeypatch.setenv(k, v)
+        kswitch(k, v)
     sdrhip = built_lib
     nstreams = 3
     rng = np.random.default_rng(7 + up)
@@ -273,14 +273,14 @@ def test_resample_many_streams(gpu_ctx, oracle, built_lib, up, down, cnt, nstrea
 @pytest.mark.parametrize("kernel", ["mfma", "dot2"])
 @pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000), (256, 8200), (8, 704),
                                     (4096, 20000)])
-def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, monkeypatch, ntaps, n, kernel):
+def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, kernel):
     """BASELINE config 5's fp16 arm (fp16 storage, fp32 accumulation -- the
     Toeplitz-GEMM v_mfma_f32_32x32x16_f16 kernel for T % 8 == 0, else / under
     SDR_F16_MFMA=0 the v_dot2_f32_f16 kernel): within 2^-9 * sum|h| * max|x|
     of the exact fp32 reference, and within fp32 accumulation error of the
     exact sum over the fp16-rounded operands.  The carried fp16 state is the
     last ns inputs, exactly."""
-    monkeypatch.setenv("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
+    kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(ntaps + n)
     h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
@@ -312,11 +312,11 @@ def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, monkeypatch, ntaps,
 
 
 @pytest.mark.parametrize("kernel", ["mfma", "dot2"])
-def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, monkeypatch, kernel):
+def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, kswitch, kernel):
     """The fp16 arm on padded rows (x_stride, y_stride > n) over 3 streams, two
     blocks: each stream within the tolerance of its own exact fp32 filter, the
     padding never written, the fp16 state exact."""
-    monkeypatch.setenv("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
+    kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(77)
     ntaps, n, nstreams = 1024, 20000, 3
@@ -348,16 +348,16 @@ def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, monkeypatch, kern
 @pytest.mark.parametrize("waves", ["8", "4"])
 @pytest.mark.parametrize("head", ["1", "0"])
 @pytest.mark.parametrize("ns", [1500, 5000])
-def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, monkeypatch, ns, head, waves):
+def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, kswitch, ns, head, waves):
     """The MFMA fp16 arm with a carried state longer than T-1 (the first
     workgroup stages positions [-T, 0) of it and rewrites all ns, past its
     register slots through its loop), under both state-staging orders
     (SDR_F16_HEAD) and both workgroup shapes (SDR_F16_W8: 8 waves of one tile,
     4 of two), two blocks: within the tolerance of the exact fp32 filter, the
     state exact."""
-    monkeypatch.setenv("SDR_F16_MFMA", "1")
-    monkeypatch.setenv("SDR_F16_HEAD", head)
-    monkeypatch.setenv("SDR_F16_W8", "1" if waves == "8" else "0")
+    kswitch("SDR_F16_MFMA", "1")
+    kswitch("SDR_F16_HEAD", head)
+    kswitch("SDR_F16_W8", "1" if waves == "8" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(ns)
     ntaps, n, nstreams = 1024, 20000, 2
@@ -391,13 +391,13 @@ def _fm_streams(nstreams, n, seed=5):
 
 @pytest.mark.parametrize("src", ["f32", "f32sc", "u8", "u8sc"])
 @pytest.mark.parametrize("D,n", [(10, 65540), (10, 5120), (5, 40960)])
-def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, monkeypatch, src, D, n):
+def test_frontend_batched_vs_oracle(gpu_ctx, oracle, built_lib, kswitch, src, D, n):
     """nstreams independent streams x 3 consecutive blocks through the
     device-resident batched call; every stream checked against the oracle.
     f32sc: the f32 call on fir_tile_sc (SDR_FIR_SC=1)."""
     sdrhip = built_lib
-    monkeypatch.setenv("SDR_FIR_SC", "1" if src == "f32sc" else "0")
-    monkeypatch.setenv("SDR_FIR_SC_U8", "1" if src == "u8sc" else "0")
+    kswitch("SDR_FIR_SC", "1" if src == "f32sc" else "0")
+    kswitch("SDR_FIR_SC_U8", "1" if src == "u8sc" else "0")
     src = src[:-2] if src.endswith("sc") else src
     nstreams, nblk = 6, 3
     h = load_golden("taps")["lpf_rf_mode0" if D == 10 else "lpf_rf_mode1"]
@@ -645,7 +645,7 @@ def test_pll_many_streams_vs_oracle(gpu_ctx, oracle, built_lib, mix, n):
 
 @pytest.mark.parametrize("trig0,phase0", [(0.0, 0.0), (3.0e6, 0.0), (1.6e7, 0.0), (16773000.0, 0.0),
                                           (16777216.0, 0.0), (16777216.0, 2.5e7)])
-def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, phase0, monkeypatch):
+def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, phase0, kswitch):
     """The PLL kernel's certified short-chain path (csrc/pll_fast.hpp, the
     default) against its library-routine path (SDR_PLL_FAST=0) on 512 streams
     x 8,192 samples, bitwise, and 8 streams of it against the oracle.  trig0
@@ -668,7 +668,7 @@ def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, phase0, monkeypa
     d_x = A.from_numpy(gpu_ctx, x)
     res = {}
     for fast in ("1", "0"):
-        monkeypatch.setenv("SDR_PLL_FAST", fast)
+        kswitch("SDR_PLL_FAST", fast)
         d_pll = A.from_numpy(gpu_ctx, st0)
         d_out = A(gpu_ctx, S * n * 4)
         gpu_ctx.fm_pll_dev(d_x, n, S, n, 19e3, Fs, 2.0, 0.0, 0.01, d_pll, None, n, d_out, n)
@@ -684,7 +684,7 @@ def test_pll_fast_vs_library(gpu_ctx, oracle, built_lib, trig0, phase0, monkeypa
 
 
 @pytest.mark.parametrize("guard,n", [("1", 4096), ("0", 4096), ("1", 4093)])
-def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch, guard, n):
+def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, kswitch, guard, n):
     """The certified path (its rotation phase detector, the 1,024-ulp window
     and the chunk guards) on inputs far from a pilot: magnitudes 2^-40..2^40
     with random signs, 2 % exact zeros, 1 % tiny or subnormal samples
@@ -693,7 +693,7 @@ def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch
     guard: the chunks' input checks from the parallel pre-pass (1, default)
     or inside the recurrence (SDR_PLL_GUARD=0); n = 4093 leaves a ragged tail."""
     sdrhip = built_lib
-    monkeypatch.setenv("SDR_PLL_GUARD", guard)
+    kswitch("SDR_PLL_GUARD", guard)
     rng = np.random.default_rng(11)
     S, Fs = 256, 240e3
     x = (rng.choice([-1.0, 1.0], (S, n)) * np.exp2(rng.uniform(-40, 40, (S, n)))).astype(np.float32)
@@ -710,7 +710,7 @@ def test_pll_fast_vs_library_wild_inputs(gpu_ctx, oracle, built_lib, monkeypatch
     d_x = A.from_numpy(gpu_ctx, x)
     res = {}
     for fast in ("1", "0"):
-        monkeypatch.setenv("SDR_PLL_FAST", fast)
+        kswitch("SDR_PLL_FAST", fast)
         d_pll = A.from_numpy(gpu_ctx, st0)
         d_out = A(gpu_ctx, S * n * 4)
         gpu_ctx.fm_pll_dev(d_x, n, S, n, 19e3, Fs, 2.0, 0.0, 0.01, d_pll, None, n, d_out, n)
@@ -754,3 +754,147 @@ def test_resample_plan_vs_oracle(gpu_ctx, oracle, built_lib, up, down, cnt, ns, 
             assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
     finally:
         plan.close()
+
+
+# ------------------------------------------------ non-finite inputs (VERDICT r4)
+
+def _rows(a, stride):
+    """[S][n] -> [S][stride] zero-padded rows (stride > n: padded or misaligned rows)."""
+    out = np.zeros((a.shape[0], stride), np.float32)
+    out[:, :a.shape[1]] = a
+    return out
+
+
+@pytest.mark.parametrize("kernel", ["sc", "tile", "generic"])
+def test_frontend_nonfinite_inputs(gpu_ctx, built_lib, kswitch, kernel):
+    """The fused front end (src/filter.cpp:123-140 x2 + 85-102) on the
+    compiled reference's non-finite fixture: Inf, -Inf and NaN in I, in Q, in
+    the carried state and prev_*, at a stream's first tile, mid-block, in the
+    last 3 samples and in the second block's first tile, and finite inputs
+    whose sums overflow to +-Inf (Inf envelopes, Inf - Inf).  7 streams in one
+    batched launch, two blocks of 5,130 pairs (n % 4 = 2: the straddling
+    chunk); fir_tile_sc (default), fir_tile, and the generic kernel (rows not
+    16-B aligned).  Outputs and every carried word bitwise where the
+    reference's is a number or an infinity, NaN where it is NaN."""
+    from conftest import assert_bits_nan
+
+    sdrhip = built_lib
+    kswitch("SDR_FIR_SC", 0 if kernel == "tile" else 1)
+    g = load_golden("nonfinite_frontend")
+    S, nblk, nout = g["demod"].shape
+    block = g["I"].shape[1] // nblk
+    stride = block + (1 if kernel == "generic" else 2)
+    A = sdrhip.DeviceArray
+    d_h = A.from_numpy(gpu_ctx, g["h"])
+    d_si, d_sq = A.from_numpy(gpu_ctx, g["state_i0"]), A.from_numpy(gpu_ctx, g["state_q0"])
+    d_pi = A.from_numpy(gpu_ctx, np.ascontiguousarray(g["prev0"][:, 0]))
+    d_pq = A.from_numpy(gpu_ctx, np.ascontiguousarray(g["prev0"][:, 1]))
+    d_out = A(gpu_ctx, S * nout * 4)
+    for b in range(nblk):
+        sl = slice(b * block, (b + 1) * block)
+        d_I = A.from_numpy(gpu_ctx, _rows(g["I"][:, sl], stride))
+        d_Q = A.from_numpy(gpu_ctx, _rows(g["Q"][:, sl], stride))
+        gpu_ctx.frontend_dev(10, d_I, d_Q, block, S, stride, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
+        gpu_ctx.synchronize()
+        got = d_out.download().reshape(S, nout)
+        for s in range(S):
+            assert_bits_nan(got[s], g["demod"][s, b], f"{kernel} stream {s} block {b}")
+        st = g["states"][:, b]
+        assert_bits_nan(d_si.download().reshape(S, 100), st[:, :100], f"{kernel} state_i block {b}")
+        assert_bits_nan(d_sq.download().reshape(S, 100), st[:, 100:200], f"{kernel} state_q block {b}")
+        assert_bits_nan(d_pi.download(), st[:, 200], f"{kernel} prev_i block {b}")
+        assert_bits_nan(d_pq.download(), st[:, 201], f"{kernel} prev_q block {b}")
+
+
+# kernel: which path runs the fixture (rows 16-B aligned or not, switches)
+NONFINITE_FIR = [("nonfinite_fir_101", "tileD1"), ("nonfinite_fir_101", "generic"),
+                 ("nonfinite_fir_1024", "long"), ("nonfinite_fir_1024", "long_sgpr"),
+                 ("nonfinite_fir_100", "generic"), ("nonfinite_decim_101", "grp"),
+                 ("nonfinite_decim_101", "generic")]
+
+
+@pytest.mark.parametrize("name,kernel", NONFINITE_FIR)
+def test_fir_block_nonfinite_inputs(gpu_ctx, built_lib, manifest, kswitch, name, kernel):
+    """blockConvolveFIR (src/filter.cpp:66-83) and the single-channel
+    downsampleBlockConvolveFIR (:123-140) on the reference's non-finite
+    fixtures: Inf / NaN in samples and carried state (first sample, mid-block,
+    the block's last sample carried on, the state's newest word) and sums
+    overflowing to +-Inf, 4 streams x 2 blocks in one batched launch each, on
+    every kernel the shape can take: fir_tile D = 1 (101 taps), fir_long with
+    LDS or SGPR taps (1024), the persistent fir_tile_grp (D = 10), and
+    fir_generic (100 taps, or rows not 16-B aligned)."""
+    from conftest import assert_bits_nan
+
+    sdrhip = built_lib
+    kswitch("SDR_LONG_VTAP", 0 if kernel == "long_sgpr" else 1)
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    S, D, block, ns, T = p["streams"], p["D"], p["block"], p["state"], p["ntaps"]
+    nout = block // D
+    stride = block + (1 if kernel == "generic" else 4)
+    A = sdrhip.DeviceArray
+    d_h = A.from_numpy(gpu_ctx, g["h"])
+    d_st = A.from_numpy(gpu_ctx, g["state0"])
+    d_y = A(gpu_ctx, S * nout * 4)
+    for b in range(p["nblk"]):
+        d_x = A.from_numpy(gpu_ctx, _rows(g["x"][:, b * block:(b + 1) * block], stride))
+        gpu_ctx.fir_decim_dev(D, d_x, block, S, stride, d_h, T, d_st, ns, d_y, nout)
+        gpu_ctx.synchronize()
+        got = d_y.download().reshape(S, nout)
+        for s in range(S):
+            assert_bits_nan(got[s], g["y"][s, b], f"{name} {kernel} stream {s} block {b}")
+        assert_bits_nan(d_st.download().reshape(S, ns), g["states"][:, b], f"{name} {kernel} state block {b}")
+
+
+def test_demod_nonfinite_inputs(gpu_ctx, built_lib, manifest):
+    """fmDemodArctan (src/filter.cpp:85-102) alone on the reference's
+    non-finite fixture: Inf / NaN in I, Q and the carried prev_*, envelopes
+    that overflow the float (2e19^2 * 2) but not the double, a zero envelope
+    between non-finite neighbours -- the `param == 0` rule (:89-92) and the
+    IEEE divide meet Inf; three calls carry prev_* on."""
+    from conftest import assert_bits_nan
+
+    sdrhip = built_lib
+    g = load_golden("nonfinite_demod")
+    A = sdrhip.DeviceArray
+    d_pi, d_pq = A.from_numpy(gpu_ctx, g["prev0"][:1]), A.from_numpy(gpu_ctx, g["prev0"][1:])
+    outs = []
+    for i, (a, b) in enumerate(manifest["cases"]["nonfinite_demod"]["params"]["segments"]):
+        d_I, d_Q = A.from_numpy(gpu_ctx, g["I"][a:b]), A.from_numpy(gpu_ctx, g["Q"][a:b])
+        d_o = A(gpu_ctx, (b - a) * 4)
+        gpu_ctx.fm_demod_dev(d_I, d_Q, b - a, 1, b - a, d_pi, d_pq, d_o, b - a)
+        gpu_ctx.synchronize()
+        outs.append(d_o.download())
+        prev = np.concatenate([d_pi.download(), d_pq.download()])
+        assert_bits_nan(prev, g["prevs"][i], f"prev after segment {i}")
+        # the same segment through the host one-block call (filter.h contract)
+        pv = (g["prev0"] if i == 0 else g["prevs"][i - 1]).copy()
+        assert_bits_nan(gpu_ctx.fm_demod(g["I"][a:b], g["Q"][a:b], pv), outs[-1], f"host call segment {i}")
+    assert_bits_nan(np.concatenate(outs), g["out"], "demod")
+
+
+def test_fir_long_8192_taps_both_tap_modes(gpu_ctx, oracle, built_lib, kswitch):
+    """fir_long at its largest tap count (8,192): the LDS-tap kernel would
+    halve the workgroups per CU there, so the launcher takes the SGPR-tap
+    kernel; under either switch setting the outputs and state are
+    bitwise the oracle's (src/filter.cpp:66-83), 2 streams x 2 blocks."""
+    sdrhip = built_lib
+    T, ns, n, S = 8192, 8191, 20000, 2
+    rng = np.random.default_rng(8192)
+    h = (rng.standard_normal(T) / T).astype(np.float32)
+    A = sdrhip.DeviceArray
+    d_h = A.from_numpy(gpu_ctx, h)
+    for vtap in (1, 0):
+        kswitch("SDR_LONG_VTAP", vtap)
+        st = rng.standard_normal((S, ns)).astype(np.float32)
+        d_st = A.from_numpy(gpu_ctx, st)
+        ost = [st[s].copy() for s in range(S)]
+        d_y = A(gpu_ctx, S * n * 4)
+        for b in range(2):
+            x = rng.standard_normal((S, n)).astype(np.float32)
+            gpu_ctx.fir_block_dev(A.from_numpy(gpu_ctx, x), n, S, n, d_h, T, d_st, ns, d_y, n)
+            gpu_ctx.synchronize()
+            got = d_y.download().reshape(S, n)
+            for s in range(S):
+                assert_bits(got[s], oracle.fir_block(x[s], h, ost[s]), f"vtap {vtap} stream {s} block {b}")
+            assert_bits(d_st.download().reshape(S, ns), np.stack(ost), f"vtap {vtap} state block {b}")

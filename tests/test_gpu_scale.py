@@ -340,25 +340,21 @@ def test_long_stream_segments_two_threads(built_lib, oracle, D, T, ns):
     assert_bits(res[1][3], pv, "prev vs the oracle")
 
 
-@pytest.mark.parametrize("stages", [2, 3])
 @pytest.mark.parametrize("graph", [False, True])
-def test_stereo_two_stage_pipeline(built_lib, oracle, graph, stages):
+def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
     """bench.py --stereo-pipeline's schedule (and sdr_project's): each block as
     sdr_stereo_front_u8_dev on one context's stream and sdr_stereo_back_dev on
     a second context's, two work objects in a ring, front(b) waiting for
     back(b-2) and back(b) for front(b) by sdr_ctx_wait_event -- block b+1's
     front overlapping block b's PLL recurrence.  128 streams x 5 mode-0
     blocks, direct or captured as one HIP graph spanning both streams:
-    every PCM byte and every carried state word against the oracle chain.
-    stages = 3: the back stage cut again after the recurrence
-    (sdr_stereo_pll_dev | sdr_stereo_post_dev on a third context), three
-    work objects in the ring -- bench.py --stereo-pipeline 2."""
+    every PCM byte and every carried state word against the oracle chain."""
     sdrhip = built_lib
     mode, nstreams, nblk = 0, 128, 5
     rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
     npairs = block_bytes // 2
     na = sdrhip.resample_out_len(up, down, npairs // D)
-    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb, sdrhip.Context(0) as cc:  # each on its own HIP stream
+    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb:  # each on its own HIP stream
         blocks = _synth_blocks(ca, sdrhip, nstreams, npairs, nblk, 777)
         A = sdrhip.DeviceArray
         d_taps = {k: A.from_numpy(ca, v) for k, v in taps.items()}
@@ -372,10 +368,9 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph, stages):
                                    d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr,
                                    d_st["stereo"].ptr, 100, d_st["pll"].ptr)
         pcm = [A(ca, nstreams * 2 * na * 2) for _ in range(nblk)]
-        ns_ = stages
+        ns_ = 2
         works = [ca.stereo_work(D, npairs, up, down, nstreams) for _ in range(ns_)]
         ev_f = [sdrhip.Event(ca) for _ in range(ns_)]
-        ev_p = [sdrhip.Event(ca) for _ in range(ns_)]
         ev_b = [sdrhip.Event(ca) for _ in range(ns_)]
 
         def run(b0, k):
@@ -386,15 +381,8 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph, stages):
                 ca.stereo_front_u8_dev(blocks[b][0], 2 * npairs, t, state, works[slot])
                 ev_f[slot].record(ca)
                 ev_f[slot].wait(cb)
-                if stages == 3:
-                    cb.stereo_pll_dev(audio_fs, state, works[slot])
-                    ev_p[slot].record(cb)
-                    ev_p[slot].wait(cc)
-                    cc.stereo_post_dev(t, state, works[slot], pcm[b], 2 * na)
-                    ev_b[slot].record(cc)
-                else:
-                    cb.stereo_back_dev(audio_fs, t, state, works[slot], pcm[b], 2 * na)
-                    ev_b[slot].record(cb)
+                cb.stereo_back_dev(audio_fs, t, state, works[slot], pcm[b], 2 * na)
+                ev_b[slot].record(cb)
             ev_b[(b0 + k - 1) % ns_].wait(ca)
 
         try:
@@ -407,7 +395,6 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph, stages):
                 run(1, nblk - 1)
             ca.synchronize()
             cb.synchronize()
-            cc.synchronize()
             if graph:
                 g.close()
             ost = [_stereo_state0() for _ in range(nstreams)]
@@ -425,5 +412,103 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph, stages):
         finally:
             for w in works:
                 w.close()
-            for e in ev_f + ev_p + ev_b:
+            for e in ev_f + ev_b:
                 e.close()
+
+
+def _stereo_state_dev(ctx, sdrhip, nstreams):
+    A = sdrhip.DeviceArray
+    st0 = _stereo_state0()
+    d_st = {k: A.from_numpy(ctx, np.tile(v, nstreams)) for k, v in st0.items() if k != "prev"}
+    d_pi = A.from_numpy(ctx, np.zeros(nstreams, np.float32))
+    d_pq = A.from_numpy(ctx, np.zeros(nstreams, np.float32))
+    state = sdrhip.StereoState(d_st["i"].ptr, d_st["q"].ptr, 100, d_pi.ptr, d_pq.ptr, d_st["delay"].ptr, 50,
+                               d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr, d_st["stereo"].ptr,
+                               100, d_st["pll"].ptr)
+    return state, [d_st, d_pi, d_pq]
+
+
+def test_stereo_work_destroy_waits_for_other_context(built_lib, oracle):
+    """a stereo work created on context A whose back stage is still
+    queued on context B is destroyed through A.  sdr_stereo_work_destroy must
+    wait for B's stream (it records an event on every stream a stage ran on),
+    so the freed buffers -- immediately re-allocated and overwritten on A's
+    stream -- are not in use: the PCM equals the one-call path's bit for bit."""
+    sdrhip = built_lib
+    mode, nstreams = 0, 8192  # a back stage of a few ms: long enough to still be queued at destroy
+    rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
+    npairs = block_bytes // 2
+    nd = npairs // D
+    na = sdrhip.resample_out_len(up, down, nd)
+    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb:
+        A = sdrhip.DeviceArray
+        (d_iq, _), = _synth_blocks(ca, sdrhip, nstreams, npairs, 1, 99)
+        d_taps = {k: A.from_numpy(ca, v) for k, v in taps.items()}
+        t = sdrhip.StereoTaps(d_taps["rf"].ptr, 101, d_taps["audio"].ptr, len(taps["audio"]), d_taps["pilot"].ptr,
+                              d_taps["stereo"].ptr, 101)
+        # reference: the one-call path on a fresh state
+        st_ref, keep_ref = _stereo_state_dev(ca, sdrhip, nstreams)
+        pcm_ref = A(ca, nstreams * 2 * na * 2)
+        ca.stereo_pcm_u8_dev(D, d_iq, npairs, nstreams, 2 * npairs, up, down, audio_fs, t, st_ref, pcm_ref, 2 * na)
+        ca.synchronize()
+        want = pcm_ref.download(np.int16)
+        # the two-stage path, destroyed while B's back stage is queued
+        st, keep = _stereo_state_dev(ca, sdrhip, nstreams)
+        pcm = A(ca, nstreams * 2 * na * 2)
+        pcm.fill(0)
+        ev = sdrhip.Event(ca)
+        w = ca.stereo_work(D, npairs, up, down, nstreams)
+        ca.stereo_front_u8_dev(d_iq, 2 * npairs, t, st, w)
+        ev.record(ca)
+        ev.wait(cb)
+        cb.stereo_back_dev(audio_fs, t, st, w, pcm, 2 * na)
+        w.close()  # through A, while B may still be running the back stage
+        d4, a4, p4 = (nd + 3) // 4 * 4, (na + 3) // 4 * 4, (nd + 4) // 4 * 4
+        junk = A(ca, 4 * nstreams * (5 * d4 + 2 * a4 + p4) + nstreams * nd)
+        junk.fill(0xFF)  # NaN patterns over whatever was freed
+        ca.synchronize()
+        cb.synchronize()
+        got = pcm.download(np.int16)
+        assert np.array_equal(got, want), "PCM after destroying the work mid-flight differs"
+        ev.close()
+        junk.free()
+
+
+def test_resample_plan_destroy_waits_for_other_context(built_lib, oracle):
+    """a resampler plan created on context A, its launch queued on
+    context B, destroyed through A: destroy waits for B's launch (per-stream
+    events) before freeing the tables, which are then re-allocated and
+    overwritten; the outputs equal a run whose plan outlived it."""
+    sdrhip = built_lib
+    up, down, T, S, n, ns = 147, 800, 151 * 147, 1024, 65600, 150
+    ny = sdrhip.resample_out_len(up, down, n)
+    h = oracle.taps_lpf(240e3 * 147, 16e3, T, 147)
+    with sdrhip.Context(0) as ca, sdrhip.Context(0) as cb:
+        A = sdrhip.DeviceArray
+        d_h = A.from_numpy(ca, h)
+        d_x = A(ca, S * n * 4)
+        d_iq = A(ca, S * 2 * n)
+        ca.synth_fm_u8_dev(d_iq, n, S, 2 * n, seed=5)
+        d_q = A(ca, S * n * 4)
+        ca.u8_to_planar_dev(d_iq, n, S, 2 * n, d_x, d_q, n)
+        ca.synchronize()
+        outs = []
+        for early in (False, True):
+            d_st = A.from_numpy(ca, np.zeros(S * ns, np.float32))
+            d_y = A(ca, S * ny * 4)
+            plan = ca.resample_plan(up, down, d_h, T)
+            for _ in range(3):  # three launches queued on B
+                plan_ctx = sdrhip.ResamplePlan(cb, plan._p)
+                plan_ctx.resample_dev(d_x, n, S, n, d_st, ns, d_y, ny)
+            if early:
+                plan.close()  # through A while B's launches may still run
+                junk = A(ca, 4 * 4 * 147 * 160 + 4096)
+                junk.fill(0xFF)
+            cb.synchronize()
+            if not early:
+                plan.close()
+            else:
+                junk.free()
+            outs.append((d_y.download(), d_st.download()))
+        assert_bits(outs[1][0], outs[0][0], "outputs with the plan destroyed mid-flight")
+        assert_bits(outs[1][1], outs[0][1], "state with the plan destroyed mid-flight")

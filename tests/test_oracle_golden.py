@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, assert_bits, load_golden
+from conftest import GOLDEN, assert_bits, assert_bits_nan, load_golden
 
 
 def test_manifest_hashes(manifest):
@@ -147,3 +147,43 @@ def test_oracle_vs_compiled_reference_random(oracle):
     s1 = rng.standard_normal(150).astype(np.float32)
     s2 = s1.copy()
     assert_bits(oracle.resample(3, 8, x, hh, s1), ref.resample(3, 8, x, hh, s2), "resample 3/8")
+
+
+def test_nonfinite_frontend(oracle):
+    """Inf / NaN in samples, carried state and prev_*, sums overflowing to
+    Inf: the oracle propagates them as the compiled reference did."""
+    g = load_golden("nonfinite_frontend")
+    S, nblk, block = g["demod"].shape[0], g["demod"].shape[1], g["I"].shape[1] // g["demod"].shape[1]
+    for s in range(S):
+        si, sq, prev = g["state_i0"][s].copy(), g["state_q0"][s].copy(), g["prev0"][s].copy()
+        for b in range(nblk):
+            sl = slice(b * block, (b + 1) * block)
+            yi = oracle.fir_decim(10, g["I"][s, sl], g["h"], si)
+            yq = oracle.fir_decim(10, g["Q"][s, sl], g["h"], sq)
+            assert_bits_nan(oracle.fm_demod(yi, yq, prev), g["demod"][s, b], f"stream {s} block {b}")
+            assert_bits_nan(np.concatenate([si, sq, prev]), g["states"][s, b], f"stream {s} state {b}")
+    assert np.isnan(g["demod"]).any() and np.isinf(g["demod"]).any()
+
+
+@pytest.mark.parametrize("name", ["nonfinite_fir_101", "nonfinite_fir_1024", "nonfinite_fir_100",
+                                  "nonfinite_decim_101"])
+def test_nonfinite_fir(oracle, manifest, name):
+    g = load_golden(name)
+    p = manifest["cases"][name]["params"]
+    for s in range(p["streams"]):
+        st = g["state0"][s].copy()
+        for b in range(p["nblk"]):
+            xb = g["x"][s, b * p["block"]:(b + 1) * p["block"]]
+            y = oracle.fir_block(xb, g["h"], st) if p["D"] == 1 else oracle.fir_decim(p["D"], xb, g["h"], st)
+            assert_bits_nan(y, g["y"][s, b], f"{name} stream {s} block {b}")
+            assert_bits_nan(st, g["states"][s, b], f"{name} stream {s} state {b}")
+
+
+def test_nonfinite_demod(oracle, manifest):
+    g = load_golden("nonfinite_demod")
+    prev = g["prev0"].copy()
+    outs = []
+    for i, (a, b) in enumerate(manifest["cases"]["nonfinite_demod"]["params"]["segments"]):
+        outs.append(oracle.fm_demod(g["I"][a:b], g["Q"][a:b], prev))
+        assert_bits_nan(prev, g["prevs"][i], f"prev after segment {i}")
+    assert_bits_nan(np.concatenate(outs), g["out"], "demod")
