@@ -131,6 +131,14 @@ def plan_devices(gpus: int, env: dict, visible: int) -> dict:
         if gpus != world:
             raise SystemExit(f"--gpus {gpus} but WORLD_SIZE {world}: launch with --nproc-per-node {gpus}")
         local = int(env.get("LOCAL_RANK", "0"))
+        if env.get("SDR_BENCH_DEVICES"):
+            # rehearsal hook for the rank path: rank r runs device list[LOCAL_RANK]
+            # (e.g. "0,0": two ranks on a one-GPU box, the real kernels and the
+            # gloo barrier; n_gpus then counts ranks)
+            devs = [int(x) for x in env["SDR_BENCH_DEVICES"].split(",")]
+            if len(devs) != world or any(d < 0 or d >= visible for d in devs):
+                raise SystemExit(f"SDR_BENCH_DEVICES={env['SDR_BENCH_DEVICES']} does not name {world} visible devices")
+            return {"mode": "ranks", "rank": int(env.get("RANK", "0")), "world": world, "devices": [devs[local]]}
         if local >= visible:
             raise SystemExit(f"LOCAL_RANK {local} but only {visible} device(s) visible")
         return {"mode": "ranks", "rank": int(env.get("RANK", "0")), "world": world, "devices": [local]}
@@ -158,66 +166,115 @@ def aggregate(per_device_ms: list, units_per_device: int, steps: int) -> dict:
 
 
 # ----------------------------------------------------------- CPU baseline --
+# per config: the reference code the CPU baseline times (oracle/cpu_bench.cpp) and its block
+CPU_KERNELS = {
+    "cfg2": ("frontend", 65540), "cfg2u8": ("frontend", 65540), "cfg4": ("frontend", 262150),
+    "cfg4x8": ("frontend", 262150),
+    # the resampler on the bench's 65,600-sample blocks (src/filter.cpp:142-173)
+    "cfg3": ("resample", 65600),
+    # the 1024-tap block FIR on I and Q (src/filter.cpp:66-83); a 131,072-sample block keeps one
+    # block of the sample within the time budget -- the rate per pair does not depend on it
+    "cfg5": ("fir1024", 131072), "cfg5h": ("fir1024", 131072),
+    # the reference PROGRAM (src/project.cpp, mode 0), u8 IQ on stdin -> s16 PCM on stdout
+    "mono0": ("program", "mono"), "stereo0": ("program", "stereo"), "stereo0w": ("program", "stereo"),
+}
+
+
+def _host_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds: float, config: str):
     """The reference's own code timed on this host's cores by
-    the native timer oracle/cpu_bench.cpp: (i) the front end of this config's
-    workload (65,540-pair mode-0 blocks) on 1 thread and on every core of the
-    process's CPU share (the affinity set capped by the cgroup CPU quota and
-    OMP_NUM_THREADS: a GPU box grants 16 of its 256 cores), one independent
-    stream per std::thread; (ii) BASELINE
-    config 1 -- the reference program `project 0 mono` on 51,200-pair blocks
-    -- as 1 process and as one process per core.  The reference build
-    (oracle/_ref, kind 'reference') when present, else the C restatement
-    (kind 'port', front end only)."""
+    the native timer oracle/cpu_bench.cpp, for THIS config's workload:
+    (i) the config's kernel -- the mode-0 front end (cfg2/cfg2u8/cfg4/cfg4x8),
+    the 147/800 resampler (cfg3), the 1024-tap block FIR on I and Q
+    (cfg5/cfg5h) -- on 1 thread and on every core of the process's CPU share
+    (the affinity set capped by the cgroup CPU quota and OMP_NUM_THREADS: a
+    GPU box grants 16 of its 256 cores), one independent stream per
+    std::thread; or, for the program configs (mono0, stereo0, stereo0w), the
+    reference program `project 0 mono|stereo` as 1 process and as one process
+    per core; (ii) for the front-end configs also BASELINE config 1 -- the
+    reference program `project 0 mono` on 51,200-pair blocks.  The reference
+    build (oracle/_ref, kind 'reference') when present, else the C
+    restatement (kind 'port', kernels only)."""
     ref = os.path.join(REPO, "oracle", "_ref", "cpu_bench")
     port = os.path.join(REPO, "oracle", "cpu_bench_port")
     exe, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
-    if not os.path.exists(exe):
+    if not os.path.exists(exe) or config not in CPU_KERNELS:
         return None
-    cores = int(subprocess.run([exe, "cores"], capture_output=True, text=True, check=True).stdout)
-    block = 65540
+    kernel, block = CPU_KERNELS[config]
+    proj = os.path.join(REPO, "oracle", "_ref", "project_ref")
+    model = _host_model()
 
     def run(*a):
         out = subprocess.run([exe, *map(str, a)], capture_output=True, text=True, check=True, timeout=600).stdout
         return json.loads(out)
 
-    one = run("frontend", block, seconds / 4, 1)
-    share = run("frontend", block, seconds / 4, 0)
+    rate = lambda d: d["pairs"] / d["seconds"] / 1e6  # noqa: E731
+
+    def program(channel, budget):
+        """The reference program: ~budget/2 s as one process, then one process per core."""
+        p1 = run("program", proj, 300, 1, channel)
+        per_block = max(p1["seconds"], 1e-3) / 300
+        b1 = max(50, int(budget / 2 / per_block))
+        if b1 > 300:
+            p1 = run("program", proj, b1, 1, channel)
+        pn = run("program", proj, max(50, int(b1 * 0.5)), 0, channel)
+        return p1, pn
+
+    if kernel == "program":
+        if kind != "reference" or not os.path.exists(proj):
+            return None
+        p1, pn = program(block, seconds)
+        bpb = {"mono": 1024 * 2, "stereo": 1024 * 4}[block]  # PCM bytes per 51,200-pair block, mode 0
+        return {"value": round(rate(pn), 2), "unit": "MS/s", "cores": pn["procs"], "kind": kind,
+                "value_1core": round(rate(p1), 2),
+                "sample": f"the reference program `project 0 {block}` (src/project.cpp), u8 IQ on stdin in "
+                          f"51,200-pair blocks -> s16 PCM on stdout, wall clock: {p1['pairs']} IQ pairs in one "
+                          f"process, {pn['pairs']} in {pn['procs']} concurrent processes (one per CPU of the share); "
+                          f"host {model}",
+                "pcm_ok": p1["pcm_bytes"] == p1["pairs"] // 51200 * bpb and pn["pcm_bytes"] == pn["pairs"] // 51200 * bpb}
+
+    cores = int(subprocess.run([exe, "cores"], capture_output=True, text=True, check=True).stdout)
+    one = run(kernel, block, seconds / 4, 1)
+    share = run(kernel, block, seconds / 4, 0)
     # SURVEY 8(d) asks for all host cores: one thread per CPU of the affinity
     # set, even where the cgroup quota grants fewer (they then time-share)
-    many = run("frontend", block, seconds / 4, share["affinity"]) if share["affinity"] > share["threads"] else share
-    model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    rate = lambda d: d["pairs"] / d["seconds"] / 1e6  # noqa: E731
+    many = run(kernel, block, seconds / 4, share["affinity"]) if share["affinity"] > share["threads"] else share
     # the headline is the faster of the two all-core runs: on a box whose
     # cgroup quota grants fewer CPUs than its affinity set, one thread per
     # affinity CPU time-shares the quota and runs slower than the share
     best = many if rate(many) >= rate(share) else share
+    what = {"frontend": f"{block:,}-pair mode-0 blocks (101-tap FIR+dec10 on I and Q, then the discriminator: "
+                        f"src/project.cpp:86-90)",
+            "resample": f"{block:,}-sample blocks through resampleBlockConvolveFIR 147/800, 151 taps per phase "
+                        f"(src/filter.cpp:142-173); unit = input samples",
+            "fir1024": f"{block:,}-sample blocks of I and Q through blockConvolveFIR with the 1024-tap LPF "
+                       f"(src/filter.cpp:66-83); unit = IQ pairs"}[kernel]
     res = {"value": round(rate(best), 2), "unit": "MS/s", "cores": best["threads"], "kind": kind,
            "value_1core": round(rate(one), 2), "value_share": round(rate(share), 2),
            "value_affinity": round(rate(many), 2), "threads_affinity": many["threads"],
-           "sample": f"{one['pairs'] + share['pairs'] + (many['pairs'] if many is not share else 0)} IQ pairs in "
-                     f"{block:,}-pair mode-0 blocks (101-tap FIR+dec10 on I and Q, then the discriminator: "
-                     f"src/project.cpp:86-90), one independent stream per std::thread: {many['threads']} threads "
+           "sample": f"{one['pairs'] + share['pairs'] + (many['pairs'] if many is not share else 0)} units in "
+                     f"{what}, one independent stream per std::thread: {many['threads']} threads "
                      f"(every CPU of the affinity set) for {seconds / 4:.0f} s, {share['threads']} threads (the "
                      f"CPU share: affinity capped by the cgroup quota) for {seconds / 4:.0f} s and 1 thread for "
-                     f"{seconds / 4:.0f} s; host {model}",
+                     f"{seconds / 4:.0f} s (at least one block each); host {model}",
            "cpu_share": {"cores": share["threads"], "affinity": share["affinity"],
                          "cgroup_quota": share["cgroup_quota"] or None,
                          "omp_num_threads": share["omp_num_threads"] or None}}
-    proj = os.path.join(REPO, "oracle", "_ref", "project_ref")
-    if kind == "reference" and os.path.exists(proj):
+    if kernel == "frontend" and kind == "reference" and os.path.exists(proj):
         # config 1: ~1 s of the single-process program, then one process per core
-        p1 = run("program", proj, 1500, 1)
+        p1 = run("program", proj, 1500, 1, "mono")
         blocks = max(50, int(1500 * min(1.0, (seconds / 4) / max(p1["seconds"], 1e-3))))
-        pn = run("program", proj, blocks, 0)
+        pn = run("program", proj, blocks, 0, "mono")
         res["cfg1"] = {
             "workload": "BASELINE config 1: the reference program `project 0 mono` (src/project.cpp), u8 IQ on "
                         "stdin in 51,200-pair blocks -> s16 PCM on stdout, wall clock",
@@ -668,7 +725,8 @@ def main(argv=None):
         finally:
             dist.destroy_process_group()
         results = [r]
-        distinct = world
+        distinct = len(set(int(x) for x in os.environ["SDR_BENCH_DEVICES"].split(","))) \
+            if os.environ.get("SDR_BENCH_DEVICES") else world
         per_ms = [float(x[0]) for x in allt]
         wall = max(float(x[1]) for x in allt)
         sus = [(float(x[2]), int(x[3])) for x in allt]
@@ -699,7 +757,7 @@ def main(argv=None):
                        "value": round(fval, 1), "ms_per_step": round(fms, 4),
                        "roofline_frac": roofline(job, fms, args.config, "fma")["frac"]}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("cfg2", "cfg2u8", "cfg4", "cfg4x8"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.config)
     if rank == 0:
         kind = job["kind"]

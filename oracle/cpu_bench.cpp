@@ -7,18 +7,26 @@
 // lies) or into cpu_bench_port (linked against liboracle.so, the C
 // restatement) when the reference is not present.
 //
-//   cpu_bench frontend <block_pairs> <seconds> <threads>
-//       the mode-0 front end (src/project.cpp:86-90: FIR+dec10 on I and Q,
-//       then fmDemodArctan) on independent synthetic streams, one stream per
-//       std::thread, one per core of the CPU share (<threads> = 0), pinned one per
-//       core when the whole affinity set is the share.
-//       Prints {"pairs":..., "seconds":..., "threads":...}.
-//   cpu_bench program <project_binary> <blocks> <procs>
+//   cpu_bench <kernel> <block> <seconds> <threads>
+//       one config's kernel on independent synthetic streams, one stream per
+//       std::thread, one per core of the CPU share (<threads> = 0), pinned one
+//       per core when the whole affinity set is the share; block after block
+//       with the state carried, until <seconds> have passed (at least one
+//       block).  <kernel>:
+//         frontend  the mode-0 front end (src/project.cpp:86-90: FIR+dec10 on
+//                   I and Q, then fmDemodArctan); unit = IQ pairs (cfg2, cfg4)
+//         resample  resampleBlockConvolveFIR 147/800 with 151 taps per phase
+//                   (src/filter.cpp:142-173, impulseResponseLPF(240e3*147,
+//                   16e3, 22197, 147), state 150); unit = input samples (cfg3)
+//         fir1024   blockConvolveFIR with the 1024-tap LPF on I and Q
+//                   (src/filter.cpp:66-83, state 1023); unit = IQ pairs (cfg5)
+//       Prints {"pairs":..., "seconds":..., "threads":...} (pairs = units).
+//   cpu_bench program <project_binary> <blocks> <procs> [mono|stereo]
 //       BASELINE config 1: `<project_binary> 0 mono` (the reference program,
-//       src/project.cpp) run as <procs> concurrent child processes, each fed
-//       <blocks> 102,400-byte u8 IQ blocks on stdin (51,200 pairs,
-//       src/project.cpp:188) while its PCM is drained from stdout.  Wall
-//       clock from spawn to the last exit.  Prints
+//       src/project.cpp; `stereo` for its stereo path) run as <procs>
+//       concurrent child processes, each fed <blocks> 102,400-byte u8 IQ
+//       blocks on stdin (51,200 pairs, src/project.cpp:188) while its PCM is
+//       drained from stdout.  Wall clock from spawn to the last exit.  Prints
 //       {"pairs":..., "seconds":..., "procs":..., "pcm_bytes":...}.
 //   cpu_bench cores
 //       Prints the CPU share: the affinity set (sched_getaffinity) capped by
@@ -52,6 +60,12 @@ void* ref_front_new(const float* h, int nh, int ns);
 void ref_front_free(void* p);
 long ref_front_run(void* p, int D, const float* I, const float* Q, long n, float* demod);
 long ref_taps_lpf(float Fs, float Fc, unsigned short T, int up, float* h);
+void* ref_resample_new(int up, int down, const float* h, int nh, int ns);
+void ref_resample_free(void* p);
+long ref_resample_run(void* p, const float* x, long n, float* y);
+void* ref_block_new(const float* h, int nh, int ns);
+void ref_block_free(void* p);
+long ref_block_run(void* p, const float* I, const float* Q, long n, float* yi, float* yq);
 }
 #else
 // the C restatement (liboracle.so) when the reference was not built
@@ -78,6 +92,45 @@ static long ref_front_run(void* p, int D, const float* I, const float* Q, long n
                      &f->pi, &f->pq, f->yi.data(), f->yq.data(), demod);
 }
 static long ref_taps_lpf(float Fs, float Fc, unsigned short T, int up, float* h) { return or_taps_lpf(Fs, Fc, T, up, h); }
+namespace {
+struct PortResample {
+  int up, down;
+  std::vector<float> h, st, y;
+};
+struct PortBlock {
+  std::vector<float> h, si, sq, yi, yq;
+};
+}  // namespace
+static void* ref_resample_new(int up, int down, const float* h, int nh, int ns) {
+  auto* r = new PortResample;
+  r->up = up;
+  r->down = down;
+  r->h.assign(h, h + nh);
+  r->st.assign(ns, 0.0f);
+  return r;
+}
+static void ref_resample_free(void* p) { delete static_cast<PortResample*>(p); }
+static long ref_resample_run(void* p, const float* x, long n, float*) {
+  auto* r = static_cast<PortResample*>(p);
+  r->y.resize(or_resample_len(r->up, r->down, n) + 1);
+  return or_resample(r->up, r->down, x, n, r->h.data(), (int)r->h.size(), r->st.data(), (int)r->st.size(),
+                     r->y.data());
+}
+static void* ref_block_new(const float* h, int nh, int ns) {
+  auto* r = new PortBlock;
+  r->h.assign(h, h + nh);
+  r->si.assign(ns, 0.0f);
+  r->sq.assign(ns, 0.0f);
+  return r;
+}
+static void ref_block_free(void* p) { delete static_cast<PortBlock*>(p); }
+static long ref_block_run(void* p, const float* I, const float* Q, long n, float*, float*) {
+  auto* r = static_cast<PortBlock*>(p);
+  r->yi.resize(n);
+  r->yq.resize(n);
+  or_fir_block(I, n, r->h.data(), (int)r->h.size(), r->si.data(), (int)r->si.size(), r->yi.data());
+  return or_fir_block(Q, n, r->h.data(), (int)r->h.size(), r->sq.data(), (int)r->sq.size(), r->yq.data());
+}
 #endif
 
 extern char** environ;
@@ -159,12 +212,24 @@ std::vector<unsigned char> synth_u8(long pairs, unsigned seed) {
   return iq;
 }
 
-int run_frontend(long n, double seconds, int threads) {
+enum Kind { kFrontend, kResample, kFir1024 };
+
+int run_kernel(Kind kind, long n, double seconds, int threads) {
   const std::vector<int> cpus = affinity_cpus();
   const Share share = cpu_share();
   if (threads <= 0) threads = share.cores;
-  std::vector<float> h(101);
-  ref_taps_lpf(2.4e6f, 100e3f, 101, 1, h.data());
+  // the taps the bench's config designs (impulseResponseLPF, src/filter.cpp:14-29)
+  std::vector<float> h;
+  if (kind == kFrontend) {
+    h.resize(101);
+    ref_taps_lpf(2.4e6f, 100e3f, 101, 1, h.data());
+  } else if (kind == kResample) {
+    h.resize(151 * 147);
+    ref_taps_lpf(240e3f * 147, 16e3f, 151 * 147, 147, h.data());
+  } else {
+    h.resize(1024);
+    ref_taps_lpf(2.4e6f, 100e3f, 1024, 1, h.data());
+  }
   // 4 blocks per thread (planar float, the filter.h boundary), as
   // src/iofunc.cpp:113-119 + src/project.cpp:78-81 produce them
   std::vector<std::vector<float>> I(4 * threads), Q(4 * threads);
@@ -193,7 +258,9 @@ int run_frontend(long n, double seconds, int threads) {
         CPU_SET(cpus[t % cpus.size()], &one);
         pthread_setaffinity_np(pthread_self(), sizeof one, &one);
       }
-      void* f = ref_front_new(h.data(), 101, 100);
+      void* f = kind == kFrontend   ? ref_front_new(h.data(), 101, 100)
+                : kind == kResample ? ref_resample_new(147, 800, h.data(), (int)h.size(), 150)
+                                    : ref_block_new(h.data(), 1024, 1023);
       std::vector<float> demod(n / 10);
       ready.fetch_add(1);
       while (!go.load()) std::this_thread::yield();
@@ -202,14 +269,26 @@ int run_frontend(long n, double seconds, int threads) {
       int b = 0;
       double el = 0;
       do {
-        ref_front_run(f, 10, I[4 * t + b].data(), Q[4 * t + b].data(), n, demod.data());
+        const float* xi = I[4 * t + b].data();
+        const float* xq = Q[4 * t + b].data();
+        if (kind == kFrontend)
+          ref_front_run(f, 10, xi, xq, n, demod.data());
+        else if (kind == kResample)
+          ref_resample_run(f, xi, n, nullptr);  // the IF (one channel: the demodulated stream)
+        else
+          ref_block_run(f, xi, xq, n, nullptr, nullptr);
         done += n;
         b = (b + 1) & 3;
         el = std::chrono::duration<double>(clk::now() - t0).count();
       } while (el < seconds);
       pairs[t] = done;
       secs[t] = el;
-      ref_front_free(f);
+      if (kind == kFrontend)
+        ref_front_free(f);
+      else if (kind == kResample)
+        ref_resample_free(f);
+      else
+        ref_block_free(f);
     });
   }
   while (ready.load() < threads) std::this_thread::yield();
@@ -227,7 +306,7 @@ int run_frontend(long n, double seconds, int threads) {
   return 0;
 }
 
-int run_program(const char* prog, long blocks, int procs) {
+int run_program(const char* prog, long blocks, int procs, const char* channel) {
   const long block_bytes = 1024L * 5 * 10 * 2;  // src/project.cpp:188 (mode 0)
   // 16 distinct blocks, cycled
   const std::vector<unsigned char> pool = synth_u8(16 * block_bytes / 2, 7);
@@ -251,7 +330,8 @@ int run_program(const char* prog, long blocks, int procs) {
     posix_spawn_file_actions_addclose(&fa, pout[0]);
     // the program's per-block progress lines (src/project.cpp) go nowhere
     posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
-    char a0[] = "project", a1[] = "0", a2[] = "mono";
+    char a0[] = "project", a1[] = "0", a2[16];
+    std::snprintf(a2, sizeof a2, "%s", channel);
     char* argv[] = {a0, a1, a2, nullptr};
     if (posix_spawn(&kids[p].pid, prog, &fa, nullptr, argv, environ) != 0) return 3;
     posix_spawn_file_actions_destroy(&fa);
@@ -304,16 +384,22 @@ int main(int argc, char** argv) {
     std::printf("%d\n", cpu_share().cores);
     return 0;
   }
-  if (argc == 5 && !std::strcmp(argv[1], "frontend"))
-    return run_frontend(std::atol(argv[2]), std::atof(argv[3]), std::atoi(argv[4]));
-  if (argc == 5 && !std::strcmp(argv[1], "program")) {
+  if (argc == 5 && (!std::strcmp(argv[1], "frontend") || !std::strcmp(argv[1], "resample") ||
+                    !std::strcmp(argv[1], "fir1024"))) {
+    const Kind k = !std::strcmp(argv[1], "frontend") ? kFrontend : !std::strcmp(argv[1], "resample") ? kResample
+                                                                                                      : kFir1024;
+    return run_kernel(k, std::atol(argv[2]), std::atof(argv[3]), std::atoi(argv[4]));
+  }
+  if ((argc == 5 || argc == 6) && !std::strcmp(argv[1], "program")) {
     int procs = std::atoi(argv[4]);
     if (procs <= 0) procs = cpu_share().cores;
-    return run_program(argv[2], std::atol(argv[3]), procs);
+    const char* ch = argc == 6 ? argv[5] : "mono";
+    if (std::strcmp(ch, "mono") && std::strcmp(ch, "stereo")) return 2;
+    return run_program(argv[2], std::atol(argv[3]), procs, ch);
   }
   std::fprintf(stderr,
-               "usage: cpu_bench frontend <block_pairs> <seconds> <threads|0>\n"
-               "       cpu_bench program <project_binary> <blocks> <procs|0>\n"
+               "usage: cpu_bench frontend|resample|fir1024 <block> <seconds> <threads|0>\n"
+               "       cpu_bench program <project_binary> <blocks> <procs|0> [mono|stereo]\n"
                "       cpu_bench cores\n");
   return 2;
 }

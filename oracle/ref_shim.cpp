@@ -159,4 +159,56 @@ long ref_front_run(void* p, int D, const float* I, const float* Q, long n, float
   return (long)f->dm.size();
 }
 
+// The resampler (src/filter.cpp:142-173, cfg3) and the 1024-tap block FIR on
+// I and Q (:66-83, cfg5), block after block with persistent vectors, for the
+// CPU baseline of those configs.
+struct ref_resample_state {
+  int up = 1, down = 1;
+  std::vector<float> h, st, x, y;
+};
+
+void* ref_resample_new(int up, int down, const float* h, int nh, int ns) {
+  auto* r = new ref_resample_state();
+  r->up = up;
+  r->down = down;
+  r->h.assign(h, h + nh);
+  r->st.assign(ns, 0.0f);
+  return r;
+}
+
+void ref_resample_free(void* p) { delete static_cast<ref_resample_state*>(p); }
+
+long ref_resample_run(void* p, const float* x, long n, float* y) {
+  auto* r = static_cast<ref_resample_state*>(p);
+  r->x.assign(x, x + n);
+  resampleBlockConvolveFIR(r->up, r->down, r->y, r->x, r->h, r->st);
+  if (y) out(r->y, y);
+  return (long)r->y.size();
+}
+
+struct ref_block_state {
+  std::vector<float> h, si, sq, xi, xq, yi, yq;
+};
+
+void* ref_block_new(const float* h, int nh, int ns) {
+  auto* r = new ref_block_state();
+  r->h.assign(h, h + nh);
+  r->si.assign(ns, 0.0f);
+  r->sq.assign(ns, 0.0f);
+  return r;
+}
+
+void ref_block_free(void* p) { delete static_cast<ref_block_state*>(p); }
+
+long ref_block_run(void* p, const float* I, const float* Q, long n, float* yi, float* yq) {
+  auto* r = static_cast<ref_block_state*>(p);
+  r->xi.assign(I, I + n);
+  r->xq.assign(Q, Q + n);
+  blockConvolveFIR(r->yi, r->xi, r->h, r->si);
+  blockConvolveFIR(r->yq, r->xq, r->h, r->sq);
+  if (yi) out(r->yi, yi);
+  if (yq) out(r->yq, yq);
+  return (long)r->yi.size();
+}
+
 }  // extern "C"

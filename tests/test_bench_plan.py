@@ -42,6 +42,19 @@ def test_plan_ranks_one_device_each():
         b.plan_devices(8, env, visible=8)  # --gpus must match the launcher's world size
 
 
+def test_plan_ranks_rehearsal_hook():
+    """SDR_BENCH_DEVICES under torch.distributed.run: rank r runs device
+    list[LOCAL_RANK], so two ranks can share the one GPU of a rehearsal box."""
+    b = _bench()
+    for r in (0, 1):
+        env = {"WORLD_SIZE": "2", "RANK": str(r), "LOCAL_RANK": str(r), "SDR_BENCH_DEVICES": "0,0"}
+        assert b.plan_devices(2, env, visible=1) == {"mode": "ranks", "rank": r, "world": 2, "devices": [0]}
+    with pytest.raises(SystemExit):
+        b.plan_devices(2, {"WORLD_SIZE": "2", "LOCAL_RANK": "1", "SDR_BENCH_DEVICES": "0"}, visible=1)
+    with pytest.raises(SystemExit):
+        b.plan_devices(2, {"WORLD_SIZE": "2", "LOCAL_RANK": "1"}, visible=1)  # no hook: device 1 is not there
+
+
 def test_aggregate_is_all_units_over_the_slowest_device():
     b = _bench()
     units, steps = 1024 * 65540, 100
@@ -180,3 +193,24 @@ def test_roofline_picks_the_binding_roof():
     r = b.roofline(cfg3, 0.136, "none")
     assert r["bound"] == "valu" and r["frac"] == r["valu_frac"]
     assert r["hbm_frac"] == pytest.approx(0.29, abs=0.01)
+
+
+@pytest.mark.parametrize("config", ["cfg2", "cfg3", "cfg5h", "mono0", "stereo0"])
+def test_cpu_baseline_every_config(config):
+    """bench.py attaches the reference CPU path to every config:
+    the config's own kernel through oracle/cpu_bench (the reference's
+    filter.cpp where it was built, else the C restatement), or the reference
+    program for the program configs.  A tiny time budget here."""
+    bench = _bench()
+
+    exe_ref = os.path.join(REPO, "oracle", "_ref", "cpu_bench")
+    if config in ("mono0", "stereo0") and not os.path.exists(os.path.join(REPO, "oracle", "_ref", "project_ref")):
+        pytest.skip("the reference program is not built here")
+    res = bench.cpu_baseline(0.4, config)
+    assert res is not None and res["value"] > 0 and res["unit"] == "MS/s"
+    assert res["kind"] == ("reference" if os.path.exists(exe_ref) else "port")
+    assert res["cores"] >= 1 and res["value_1core"] > 0 and res["sample"]
+    if config in ("mono0", "stereo0"):
+        assert res["pcm_ok"]
+    if config == "cfg2":
+        assert "cfg1" in res or res["kind"] == "port"
