@@ -322,6 +322,10 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
 #ifndef SDR_LP_NT
 #define SDR_LP_NT 0
 #endif
+// SDR_LP_PIPE: the scan software-pipelined by one tap
+#ifndef SDR_LP_PIPE
+#define SDR_LP_PIPE 0
+#endif
 constexpr int kLpWaves = 7;
 constexpr int kLpSlots = 64 * kLpWaves;
 constexpr int kLpGroups = kLpSlots / 16;
@@ -505,6 +509,9 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
   }
   float acc[K];
   f4v cur[K], nxt[K];
+#if SDR_LP_PIPE
+  float prod[K];  // the products of the previous tap, summed beside the next tap's
+#endif
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     acc[k] = 0.0f;
@@ -537,7 +544,15 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
       for (int k = 0; k < K; ++k) {
         float v = cur[k][jj];
         if (edge) v = ok ? v : 0.0f;
+#if SDR_LP_PIPE
+        // the sum of the previous tap beside the product of this one: an add
+        // never waits for the multiply just before it (2K - 1 instructions
+        // apart, across chunk ends too); same terms, same order, each rounded
+        if (cc > 0 || jj < 3) asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc[k]) : "v"(prod[k]));
+        asm volatile("v_mul_f32 %0, %1, %2" : "=v"(prod[k]) : "v"(tp[u]), "v"(v));
+#else
         acc[k] = acc[k] + tp[u] * v;
+#endif
       }
     }
 #pragma unroll
@@ -547,6 +562,10 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+#if SDR_LP_PIPE
+#pragma unroll
+  for (int k = 0; k < K; ++k) asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc[k]) : "v"(prod[k]));
+#endif
   // The next item's DMAs (issued before this scan) are waited for here,
   // before the output stores: vmcnt also counts stores, so a drain after them
   // would wait out their write latency too.  (LW: the loader wave stages.)

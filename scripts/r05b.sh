@@ -1,0 +1,28 @@
+#!/bin/bash
+# r05b: resampler software-pipelined scan (ab/pipe.so) parity + same-box A/B;
+# cfg2u8 / cfg3 kernel traces, cfg2u8 HBM traffic and SQ counters of
+# fir_tile_sc<U8> (VERDICT r4 missing 3); the rank path rehearsed on one GPU
+# (two torchrun ranks, SDR_BENCH_DEVICES=0,0).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r05b; mkdir -p $OUT
+SDRHIP_LIB=$PWD/ab/pipe.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q \
+  -p no:cacheprovider --timeout 120 --timeout-method thread -k "resample or cfg3" > $OUT/pytest_pipe.log 2>&1; rc=$?
+tail -2 $OUT/pytest_pipe.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_pipe.log | head; exit $rc; }
+ARMS="tree ab/pipe.so" CFGS="cfg3" REPS=3 bash scripts/ab_libs.sh > $OUT/ab_pipe.txt 2>&1; rc=$?; cat $OUT/ab_pipe.txt; [ $rc -eq 0 ] || exit $rc
+TAG=r05b CFGS="cfg2u8 cfg3" bash scripts/prof_cfg.sh || exit 1
+export TMPDIR=/tmp
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_cfg2u8_$ctr" -o pmc \
+    -- python3 bench.py --config cfg2u8 --steps 3 --warmup 1 --warm-seconds 0 --no-cpu-baseline --no-fma-variant --no-graph --sustain-seconds 0 \
+    > /dev/null 2>> "$OUT/prof.err"
+  rc=$?; echo "pmc cfg2u8 $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+python scripts/pmc_traffic.py "$(find $OUT/pmc_cfg2u8_FETCH_SIZE -name '*counter_collection.csv' | head -1)" \
+  "$(find $OUT/pmc_cfg2u8_WRITE_SIZE -name '*counter_collection.csv' | head -1)" fir_tile_sc "$OUT/traffic_cfg2u8.json" || exit 1
+TAG=r05b/sq_cfg2u8 CFG=cfg2u8 KERNEL=fir_tile_sc bash scripts/pmc_sq.sh || exit 1
+SDR_BENCH_DEVICES=0,0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 3 > $OUT/bench_ranks2.json 2> $OUT/ranks.err; rc=$?
+tail -3 $OUT/ranks.err; cat $OUT/bench_ranks2.json; [ $rc -eq 0 ] || exit $rc
+find $OUT -name '*kernel_trace.csv' -delete
+exit 0
