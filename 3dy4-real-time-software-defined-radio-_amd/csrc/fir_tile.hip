@@ -68,6 +68,10 @@
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
+// SDR_U8_PK: fir_tile_sc's wire-byte unpack with packed FMAs (A/B)
+#ifndef SDR_U8_PK
+#define SDR_U8_PK 0
+#endif
 // SDR_SCAN_VCONST (timing builds only, wrong outputs): fir_tile_sc's scan
 // with a VGPR in place of the SGPR taps
 #ifndef SDR_SCAN_VCONST
@@ -1201,12 +1205,19 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     // per chunk; the second read hits L2) and unpack their own channel
     auto put = [&](int i, const float4& w) __attribute__((always_inline)) {
       const uint32_t bx = __float_as_uint(w.x), by = __float_as_uint(w.y);
+#if SDR_U8_PK
+      // two samples per packed FMA (v_pk_fma_f32): 6 instead of 8 per chunk
+      const f32x2 x01 = c == 0 ? u8_bytes_to_f32x2<0, 2>(bx) : u8_bytes_to_f32x2<1, 3>(bx);
+      const f32x2 x23 = c == 0 ? u8_bytes_to_f32x2<0, 2>(by) : u8_bytes_to_f32x2<1, 3>(by);
+      *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(x01.x, x01.y, x23.x, x23.y);
+#else
       if (c == 0)
         *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(u8_byte_to_f32<0>(bx), u8_byte_to_f32<2>(bx),
                                                               u8_byte_to_f32<0>(by), u8_byte_to_f32<2>(by));
       else
         *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(u8_byte_to_f32<1>(bx), u8_byte_to_f32<3>(bx),
                                                               u8_byte_to_f32<1>(by), u8_byte_to_f32<3>(by));
+#endif
     };
 #pragma unroll
     for (int it = 0; it < G::FULL; ++it) put(lane + it * NTH, v[it]);
