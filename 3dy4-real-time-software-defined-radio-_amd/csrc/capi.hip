@@ -754,6 +754,16 @@ struct StreamUses {
   }
 };
 
+// A tap plan for the fp16 arm: the MFMA kernel's eight shifted copies of
+// the reversed fp16 taps built once (src/project.cpp designs its taps once),
+// instead of in every workgroup of every call.
+struct sdr_fir_f16_plan {
+  int ntaps = 0;
+  const float* h = nullptr;
+  void* copies = nullptr;  // nullptr: the shape takes no plan (calls build per launch / run v_dot2)
+  StreamUses uses;
+};
+
 struct sdr_resample_plan {
   int up = 0, down = 0, ntaps = 0;
   const float* h = nullptr;
@@ -824,8 +834,25 @@ int sdr_resample_plan_f32_dev(sdr_ctx* c, const sdr_resample_plan* p, const floa
 
 int sdr_fir_block_f16_kernel(int ntaps) { return sdr::fir_f16_uses_mfma(ntaps) ? 1 : 0; }
 
+static int fir_block_f16(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,
+                         int ntaps, void* state, int ns, float* y, long long y_stride, const void* plan);
+
 int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,
                           int ntaps, void* state, int ns, float* y, long long y_stride) {
+  return fir_block_f16(c, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, nullptr);
+}
+
+int sdr_fir_block_f16_plan_dev(sdr_ctx* c, const sdr_fir_f16_plan* p, const void* x, long long n, int nstreams,
+                               long long x_stride, void* state, int ns, float* y, long long y_stride) {
+  if (!p) return fail(c, SDR_EINVAL, "null plan");
+  const int rc = fir_block_f16(c, x, n, nstreams, x_stride, p->h, p->ntaps, state, ns, y, y_stride, p->copies);
+  if (rc || !p->copies) return rc;
+  SDR_HIP(c, const_cast<sdr_fir_f16_plan*>(p)->uses.mark(c->cur));
+  return SDR_OK;
+}
+
+static int fir_block_f16(sdr_ctx* c, const void* x, long long n, int nstreams, long long x_stride, const float* h,
+                         int ntaps, void* state, int ns, float* y, long long y_stride, const void* plan) {
   int rc = enter(c);
   if (rc) return rc;
   if (!x || !h || !state || !y) return fail(c, SDR_EINVAL, "null pointer");
@@ -837,8 +864,47 @@ int sdr_fir_block_f16_dev(sdr_ctx* c, const void* x, long long n, int nstreams, 
     return fail(c, SDR_EINVAL, "fp16 input rows must be 16-B aligned (x_stride %% 8 == 0)");
   uint32_t* pairs = static_cast<uint32_t*>(scratch(c, kTmp, sdr::fir_long_h_pairs(ntaps) * sizeof(uint32_t)));
   if (!pairs) return scratch_fail(c, "tap pair table");
-  hipError_t e = sdr::launch_fir_long_h(x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, pairs, c->cur);
+  hipError_t e =
+      sdr::launch_fir_long_h(x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride, pairs, c->cur, plan);
   if (e != hipSuccess) return hip_fail(c, e, "fir_block_f16 launch");
+  return SDR_OK;
+}
+
+int sdr_fir_f16_plan_create(sdr_ctx* c, const float* h, int ntaps, sdr_fir_f16_plan** out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!out || !h) return fail(c, SDR_EINVAL, "null pointer");
+  *out = nullptr;
+  if (ntaps < 1) return fail(c, SDR_EINVAL, "ntaps %d < 1", ntaps);
+  auto* p = new sdr_fir_f16_plan;
+  p->ntaps = ntaps;
+  p->h = h;
+  const size_t halves = sdr::fir_f16_plan_halves(ntaps);
+  if (halves) {
+    hipError_t e = hipMalloc(&p->copies, halves * 2);
+    if (e != hipSuccess) {
+      delete p;
+      return fail(c, SDR_ENOMEM, "fp16 tap plan");
+    }
+    if ((e = sdr::build_fir_f16_plan(h, ntaps, p->copies, c->cur)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->cur)) != hipSuccess || (e = p->uses.mark(c->cur)) != hipSuccess) {
+      (void)hipFree(p->copies);
+      delete p;
+      return hip_fail(c, e, "fp16 tap plan");
+    }
+  }
+  *out = p;
+  return SDR_OK;
+}
+
+int sdr_fir_f16_plan_destroy(sdr_ctx* c, sdr_fir_f16_plan* p) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (p) {
+    p->uses.wait_and_release();
+    if (p->copies) (void)hipFree(p->copies);
+    delete p;
+  }
   return SDR_OK;
 }
 

@@ -351,12 +351,16 @@ struct MfArgs {
   int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
                           // 3 = no tap staging, 4 = no output stores
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
+  const _Float16* hplan;  // PLAN: the 8 tap copies (8 * lc halves) prebuilt by sdr_fir_f16_plan_create
 };
 
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
 
-// kMfWaves waves (4: one per SIMD, two tiles each; 8: two per SIMD, one tile each)
-template <int kMfWaves>
+// kMfWaves waves (4: one per SIMD, two tiles each; 8: two per SIMD, one tile each).
+// PLAN: the tap copies come prebuilt (a tap plan, sdr_fir_f16_plan_*), brought
+// into LDS by LDS-DMA beside the image loads -- no f32 tap loads, no reversed
+// row, no copy pass and one barrier fewer; else they are built here.
+template <int kMfWaves, bool PLAN = false>
 __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   constexpr int kMfNT = 8 / kMfWaves;           // 1,024-output tiles per wave
   typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -392,12 +396,19 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // (coalesced f32 loads); the tap copies are built from them in LDS below
   _Float16* hb = hcp + 8 * a.lc;
   const int nhb = a.lc + 40;
-  float hv[kMfTaps];
-  const int ntl = SDR_ABL(a.ablate) == 3 ? 0 : a.ntaps;  // (ablation 3: no tap loads, no copies)
+  float hv[PLAN ? 1 : kMfTaps];
+  if constexpr (PLAN) {
+    // the plan's copies: lc 16-B chunks, LDS-DMA (lane l of an instruction
+    // lands at the wave-uniform base + 16 l), waited for before the barrier
+    for (int c0 = wave * 64; c0 < a.lc; c0 += kNT)
+      if (c0 + lane < a.lc) __builtin_amdgcn_global_load_lds(a.hplan + 8 * (c0 + lane), hcp + 8 * c0, 16, 0, 0);
+  } else {
+    const int ntl = SDR_ABL(a.ablate) == 3 ? 0 : a.ntaps;  // (ablation 3: no tap loads, no copies)
 #pragma unroll
-  for (int k = 0; k < kMfTaps; ++k) {
-    const int v = tid + k * kNT - 32;
-    hv[k] = (v >= 0 && v < ntl) ? a.h[a.ntaps - 1 - v] : 0.0f;
+    for (int k = 0; k < kMfTaps; ++k) {
+      const int v = tid + k * kNT - 32;
+      hv[k] = (v >= 0 && v < ntl) ? a.h[a.ntaps - 1 - v] : 0.0f;
+    }
   }
   // the stream's first workgroup (pb = -T, T <= 4096 = kMfSt * kNT): the
   // carried state for image positions q in [-T, 0) and the new state (the
@@ -441,9 +452,13 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
       }
     }
   }
+  if constexpr (PLAN) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copies' DMAs (the barrier does not wait for them)
+  } else {
 #pragma unroll
-  for (int k = 0; k < kMfTaps; ++k)
-    if (tid + k * kNT < nhb) hb[tid + k * kNT] = (_Float16)hv[k];
+    for (int k = 0; k < kMfTaps; ++k)
+      if (tid + k * kNT < nhb) hb[tid + k * kNT] = (_Float16)hv[k];
+  }
   __syncthreads();
   // the stream's first workgroup is the only reader of the old state (staged
   // above): it writes the new one, the block's last ns inputs
@@ -456,15 +471,17 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   } else if (m0 == 0) {
     for (int i = tid; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
   }
-  const int cpr = a.lc >> 3;  // 16-B chunks per copy
-  for (int c = tid; c < (SDR_ABL(a.ablate) == 3 ? 0 : 8 * cpr); c += 64 * kMfWaves) {
-    const int q = c / cpr, w0 = 8 * (c - q * cpr);
-    half8 v;
+  if constexpr (!PLAN) {
+    const int cpr = a.lc >> 3;  // 16-B chunks per copy
+    for (int c = tid; c < (SDR_ABL(a.ablate) == 3 ? 0 : 8 * cpr); c += 64 * kMfWaves) {
+      const int q = c / cpr, w0 = 8 * (c - q * cpr);
+      half8 v;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = hb[w0 + q + k];
-    *reinterpret_cast<half8*>(hcp + q * a.lc + w0) = v;
+      for (int k = 0; k < 8; ++k) v[k] = hb[w0 + q + k];
+      *reinterpret_cast<half8*>(hcp + q * a.lc + w0) = v;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int i = lane & 31, hh = lane >> 5;
   const int q = 7 - (i & 7);                            // (-i-1) mod 8
   const _Float16* arow = hcp + q * a.lc + (8 * hh - i - 1 + 32 - q);  // + 16 s: A fragment of step s
@@ -538,6 +555,17 @@ __global__ __launch_bounds__(kWG) void build_pairs_h(const float* __restrict__ h
   hp2[d] = __builtin_bit_cast(uint32_t, v);
 }
 
+// The tap plan of fir_long_mfma<.., true>: copy q of the reversed f16 taps,
+// shifted by q halves -- plan[q*lc + w] = hr[w + q - 32], hr[v] = h[T-1-v]
+// (0 outside [0, T)) -- exactly what the kernel otherwise builds in LDS.
+__global__ __launch_bounds__(kWG) void build_mf_plan(const float* __restrict__ h, int ntaps, int lc, _Float16* plan) {
+  const int idx = blockIdx.x * kWG + threadIdx.x;
+  if (idx >= 8 * lc) return;
+  const int q = idx / lc, w = idx - q * lc;
+  const int v = w + q - 32;
+  plan[idx] = (v >= 0 && v < ntaps) ? (_Float16)h[ntaps - 1 - v] : (_Float16)0;
+}
+
 __global__ __launch_bounds__(kWG) void long_commit_h(const _Float16* __restrict__ x, long long n,
                                                      long long x_stride, _Float16* state, int ns) {
   const int s = blockIdx.y;
@@ -562,9 +590,25 @@ bool fir_f16_uses_mfma(int ntaps) {
 
 size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32); }
 
+namespace {
+int mf_kd(int ntaps) { return (ntaps + 31 + 95) / 96 * 96; }  // an even number of 3-step groups
+int mf_lc(int ntaps) { return (mf_kd(ntaps) + 40 + 7) / 8 * 8; }
+}  // namespace
+
+size_t fir_f16_plan_halves(int ntaps) {
+  return (ntaps % 8 == 0 && ntaps >= 8 && ntaps <= 4096) ? (size_t)8 * mf_lc(ntaps) : 0;
+}
+
+hipError_t build_fir_f16_plan(const float* h, int ntaps, void* plan, hipStream_t st) {
+  const int lc = mf_lc(ntaps);
+  hipLaunchKernelGGL(build_mf_plan, dim3((8 * lc + kWG - 1) / kWG), dim3(kWG), 0, st, h, ntaps, lc,
+                     static_cast<_Float16*>(plan));
+  return hipGetLastError();
+}
+
 hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
                              void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
-                             hipStream_t st) {
+                             hipStream_t st, const void* plan) {
   // the MFMA form: T % 8 == 0 keeps the staged image's 16-B chunks aligned
   // (x rows are 16-B aligned, checked by the caller); SDR_F16_MFMA=0 selects
   // the dot2 kernel below (A/B, tests)
@@ -575,8 +619,8 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.x_stride = x_stride;
     a.h = h;
     a.ntaps = ntaps;
-    a.kd = (ntaps + 31 + 95) / 96 * 96;  // an even number of 3-step groups (zero taps past the band)
-    a.lc = (a.kd + 40 + 7) / 8 * 8;
+    a.kd = mf_kd(ntaps);  // zero taps past the band
+    a.lc = mf_lc(ntaps);
     a.state = static_cast<_Float16*>(state);
     a.ns = ns;
     a.y = y;
@@ -587,18 +631,24 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.ablate = ablate;
     const int head_pre = sw(kSwF16Head);  // (switch: the tests run both orders)
     a.head_pre = head_pre;
-    // image, 8 tap copies, the reversed taps (a.lc + 40 halves)
-    const size_t lds = ((size_t)mf_pad(a.span) + 8 + 9 * (size_t)a.lc + 40) * sizeof(_Float16);
+    a.hplan = static_cast<const _Float16*>(plan);
+    // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves)
+    const size_t lds = ((size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40)) *
+                       sizeof(_Float16);
     const long long blocks = (long long)a.wg_per_stream * nstreams;
     if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
     // one launch: each stream's first workgroup commits the state itself
     // two waves per SIMD, one tile each: 8.8 vs 10.9 us per kernel on cfg5h
     // (profiles/r04y/); SDR_F16_W8=0 restores four waves of two tiles
     const int w8 = sw(kSwF16W8);
-    if (w8)
-      hipLaunchKernelGGL(fir_long_mfma<8>, dim3((unsigned)blocks), dim3(512), lds, st, a);
+    if (w8 && plan)
+      hipLaunchKernelGGL((fir_long_mfma<8, true>), dim3((unsigned)blocks), dim3(512), lds, st, a);
+    else if (w8)
+      hipLaunchKernelGGL((fir_long_mfma<8, false>), dim3((unsigned)blocks), dim3(512), lds, st, a);
+    else if (plan)
+      hipLaunchKernelGGL((fir_long_mfma<4, true>), dim3((unsigned)blocks), dim3(256), lds, st, a);
     else
-      hipLaunchKernelGGL(fir_long_mfma<4>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+      hipLaunchKernelGGL((fir_long_mfma<4, false>), dim3((unsigned)blocks), dim3(256), lds, st, a);
     return hipGetLastError();
   }
   const int len = (int)fir_long_h_pairs(ntaps);

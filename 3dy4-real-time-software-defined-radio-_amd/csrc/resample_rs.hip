@@ -326,6 +326,11 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
 #ifndef SDR_LP_PIPE
 #define SDR_LP_PIPE 0
 #endif
+// SDR_LP_SPLIT: the loader wave and the compute wave on its SIMD share the
+// next item's DMA issue
+#ifndef SDR_LP_SPLIT
+#define SDR_LP_SPLIT 0
+#endif
 constexpr int kLpWaves = 7;
 constexpr int kLpSlots = 64 * kLpWaves;
 constexpr int kLpGroups = kLpSlots / 16;
@@ -440,7 +445,7 @@ __global__ __launch_bounds__(kLpSlots) void build_lp_tables(const float* __restr
 // or past the end.
 // The staging threads: tid of nth, in waves wv of nwv (all of the compute
 // waves, or the one loader wave).
-template <int CMAX, bool DMA_FIRST = false>
+template <int CMAX, bool DMA_FIRST = false, bool EDGES = true>
 __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, int tid, int nth, int wv, int nwv,
                                          int ln) {
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
@@ -480,14 +485,16 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
   // but no longer hold back their issue by a memory latency on every
   // stream's first item
   if constexpr (DMA_FIRST) dma();
-  for (int j = tid; j < (int)jlo && j < nch; j += nth) edge(j);
-  for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += nth) edge(j);
+  if constexpr (EDGES) {
+    for (int j = tid; j < (int)jlo && j < nch; j += nth) edge(j);
+    for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += nth) edge(j);
+  }
   if constexpr (!DMA_FIRST) dma();
 }
 
 template <int CMAX, int K, int LW, int NOLDS = 0>
 __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, int it, const float (&tp)[(CMAX + 6) / 4 * 4],
-                                           int phi, int sub, int A, int ctop0, bool valid) {
+                                           int phi, int sub, int A, int ctop0, bool valid, bool drain) {
   constexpr int NC = (CMAX + 6) / 4;
   const int st = it / a.nbat, b = it - st * a.nbat;
   const int t0 = b * a.C;
@@ -568,8 +575,9 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
 #endif
   // The next item's DMAs (issued before this scan) are waited for here,
   // before the output stores: vmcnt also counts stores, so a drain after them
-  // would wait out their write latency too.  (LW: the loader wave stages.)
-  if (!LW) dma_drain();
+  // would wait out their write latency too.  (LW: the loader wave stages;
+  // `drain`: this wave issued part of the next item's DMAs, SDR_LP_SPLIT.)
+  if (!LW || drain) dma_drain();
   float* ys = a.y + (long long)st * a.y_stride;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -591,6 +599,11 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   const bool loader = LW && wv == kLpWaves;  // wave-uniform
+  // SDR_LP_SPLIT: the compute wave that shares the loader's SIMD (wave 3 and
+  // wave 7 both sit on SIMD 3, the one SIMD with a single compute wave)
+  // issues every other DMA instruction of the next item: neither wave then
+  // holds more than ~34 of an item's 67 in flight (vmcnt counts 63 at most)
+  const bool helper = LW && SDR_LP_SPLIT && wv == kLpWaves - 4;
   // items: contiguous range per workgroup
   const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
   const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
@@ -601,7 +614,9 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     if (!LW)
       lp_stage<CMAX>(a, buf, it, threadIdx.x, kLpSlots, wv, kLpWaves, ln);
     else if (loader)
-      lp_stage<CMAX, SDR_LP_EARLY != 0>(a, buf, it, ln, 64, 0, 1, ln);
+      lp_stage<CMAX, SDR_LP_EARLY != 0>(a, buf, it, ln, 64, 0, SDR_LP_SPLIT ? 2 : 1, ln);
+    else if (helper)
+      lp_stage<CMAX, true, false>(a, buf, it, ln, 64, 1, 2, ln);
   };
   // the first item's DMA runs while this lane's item and taps are loaded
   stage(bufA, i0);
@@ -650,9 +665,9 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     if (!(SDR_LP_EARLY && LW) && it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
     if (SDR_ABL(a.ablate) != 2 && !loader) {
       if (odd)
-        lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
+        lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid, helper);
       else
-        lp_compute<CMAX, K, LW, NOLDS>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
+        lp_compute<CMAX, K, LW, NOLDS>(a, bufA, it, tp, phi, sub, A, ctop0, valid, helper);
     }
     if (!LW && commit && (int)threadIdx.x < a.ns) {
       dma_drain();

@@ -175,9 +175,14 @@ hipError_t launch_fir_long(const FirLaunch& a, const float* h, hipStream_t st);
 size_t fir_long_h_pairs(int ntaps);
 // whether sdr_fir_block_f16_dev runs the MFMA kernel for ntaps (else v_dot2)
 bool fir_f16_uses_mfma(int ntaps);
+// plan: the MFMA kernel's tap copies prebuilt by build_fir_f16_plan (a tap
+// plan, fir_f16_plan_halves(ntaps) halves), or nullptr to build them per launch
 hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long x_stride, const float* h, int ntaps,
                              void* state, int ns, float* y, long long y_stride, uint32_t* scratch_pairs,
-                             hipStream_t st);
+                             hipStream_t st, const void* plan = nullptr);
+// halves of the fp16 MFMA kernel's tap plan for ntaps (0: the shape takes no plan)
+size_t fir_f16_plan_halves(int ntaps);
+hipError_t build_fir_f16_plan(const float* h, int ntaps, void* plan, hipStream_t st);
 hipError_t launch_f32_to_f16(const float* x, long long count, void* y, hipStream_t st);
 
 // Whether the tiled fast path handles (D, ntaps, ns) for this source; false

@@ -96,6 +96,9 @@ _SIGS = {
     "sdr_resample_plan_f32_dev": [_vp, _vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
     "sdr_resample_plan_destroy": [_vp, _vp],
     "sdr_fir_block_f16_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _i, _vp, _ll],
+    "sdr_fir_f16_plan_create": [_vp, _vp, _i, C.POINTER(_vp)],
+    "sdr_fir_block_f16_plan_dev": [_vp, _vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
+    "sdr_fir_f16_plan_destroy": [_vp, _vp],
     "sdr_f32_to_f16_dev": [_vp, _vp, _ll, _vp],
     "sdr_fir_block_f16_kernel": [_i],
     "sdr_delay_f32_dev": [_vp, _vp, _ll, _i, _ll, _vp, _i, _vp, _ll],
@@ -277,6 +280,22 @@ class ResamplePlan:
     def close(self):
         if self._p:
             lib().sdr_resample_plan_destroy(self._ctx._c, self._p)
+            self._p = _vp()
+
+
+class F16Plan:
+    """sdr_fir_f16_plan: fir_block_f16_dev with the MFMA kernel's tap copies built once."""
+
+    def __init__(self, ctx: "Context", p):
+        self._ctx, self._p = ctx, p
+
+    def fir_block_f16_dev(self, x, n, nstreams, x_stride, state, ns, y, y_stride):
+        self._ctx._check(lib().sdr_fir_block_f16_plan_dev(self._ctx._c, self._p, _ptr(x), n, nstreams, x_stride,
+                                                          _ptr(state), ns, _ptr(y), y_stride), "fir_block_f16_plan_dev")
+
+    def close(self):
+        if self._p:
+            lib().sdr_fir_f16_plan_destroy(self._ctx._c, self._p)
             self._p = _vp()
 
 
@@ -485,6 +504,12 @@ class Context:
         """fp16-storage arm of blockConvolveFIR (tolerance, not bit-exact)."""
         self._check(lib().sdr_fir_block_f16_dev(self._c, _ptr(x), n, nstreams, x_stride, _ptr(h), ntaps,
                                                 _ptr(state), ns, _ptr(y), y_stride), "fir_block_f16_dev")
+
+    def fir_f16_plan(self, h, ntaps) -> "F16Plan":
+        """sdr_fir_f16_plan_create: the fp16 MFMA kernel's tap copies built once from device taps h."""
+        p = _vp()
+        self._check(lib().sdr_fir_f16_plan_create(self._c, _ptr(h), ntaps, C.byref(p)), "fir_f16_plan")
+        return F16Plan(self, p)
 
     def f32_to_f16_dev(self, x, count, y):
         self._check(lib().sdr_f32_to_f16_dev(self._c, _ptr(x), count, _ptr(y)), "f32_to_f16_dev")

@@ -475,9 +475,16 @@ class Job:
                 IQhs.append(IQh)
             sth = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
             out = torch.empty(2 * n, dtype=torch.float32, device=dev)
-            self.keep += [IQhs, sth, out]
-            for IQh in IQhs:
-                steps.append(lambda IQh=IQh: ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, sth, ns, out, n))
+            # a tap plan: the MFMA kernel's fp16 tap copies built once (sdr_fir_f16_plan_create), as a
+            # streaming caller with fixed taps would; bitwise the per-call path's outputs (tests)
+            fplan = ctx.fir_f16_plan(d_h, T)
+            self.keep += [IQhs, sth, out, fplan]
+            if os.environ.get("SDR_BENCH_F16_PLAN", "1") != "0":
+                for IQh in IQhs:
+                    steps.append(lambda IQh=IQh: fplan.fir_block_f16_dev(IQh, n, 2, n, sth, ns, out, n))
+            else:  # A/B: the tap copies built in every workgroup of every call
+                for IQh in IQhs:
+                    steps.append(lambda IQh=IQh: ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, sth, ns, out, n))
             self.units = n
             self.bytes_per_pair = 2.0 * 2 + 8.0  # fp16 in, fp32 out
             self.flops_per_unit = 2.0 * 2 * T
@@ -491,7 +498,7 @@ class Job:
             ctx.fir_block_dev(IQ, n, 2, n, d_h, T, z32, ns, ref, n)
             z16 = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
             got = torch.empty(2 * n, dtype=torch.float32, device=dev)
-            ctx.fir_block_f16_dev(IQhs[0], n, 2, n, d_h, T, z16, ns, got, n)
+            fplan.fir_block_f16_dev(IQhs[0], n, 2, n, z16, ns, got, n)
             torch.cuda.synchronize(dev)
             err = float((got - ref).abs().max())
             scale = float(d_h.abs().sum()) * float(IQ.abs().max())

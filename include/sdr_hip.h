@@ -244,6 +244,19 @@ int sdr_resample_plan_destroy(sdr_ctx *ctx, sdr_resample_plan *plan);
 int sdr_fir_block_f16_kernel(int ntaps);
 int sdr_fir_block_f16_dev(sdr_ctx *ctx, const void *x, long long n, int nstreams, long long x_stride,
                           const float *h, int ntaps, void *state, int ns, float *y, long long y_stride);
+/* A tap plan for the fp16 arm: the MFMA kernel's shifted fp16 tap copies
+ * built ONCE from the device taps h (a streaming caller's taps do not change,
+ * src/project.cpp:262-266), instead of in every workgroup of every call.  h
+ * must stay valid and unchanged while the plan lives (the v_dot2 fallback and
+ * shapes without a plan read it per call).  Same outputs, state and
+ * preconditions as sdr_fir_block_f16_dev.  Destroy waits for the plan's build
+ * and every direct call on every stream that used it; graph replays of calls
+ * with the plan must have completed before it. */
+typedef struct sdr_fir_f16_plan sdr_fir_f16_plan;
+int sdr_fir_f16_plan_create(sdr_ctx *ctx, const float *h, int ntaps, sdr_fir_f16_plan **plan);
+int sdr_fir_block_f16_plan_dev(sdr_ctx *ctx, const sdr_fir_f16_plan *plan, const void *x, long long n, int nstreams,
+                               long long x_stride, void *state, int ns, float *y, long long y_stride);
+int sdr_fir_f16_plan_destroy(sdr_ctx *ctx, sdr_fir_f16_plan *plan);
 /* fp32 -> fp16 (round to nearest even), count elements, stream-ordered. */
 int sdr_f32_to_f16_dev(sdr_ctx *ctx, const float *x, long long count, void *y);
 

@@ -6,15 +6,22 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r05b; mkdir -p $OUT
-SDRHIP_LIB=$PWD/ab/pipe.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q \
-  -p no:cacheprovider --timeout 120 --timeout-method thread -k "resample or cfg3" > $OUT/pytest_pipe.log 2>&1; rc=$?
-tail -2 $OUT/pytest_pipe.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_pipe.log | head; exit $rc; }
-ARMS="tree ab/pipe.so" CFGS="cfg3" REPS=3 bash scripts/ab_libs.sh > $OUT/ab_pipe.txt 2>&1; rc=$?; cat $OUT/ab_pipe.txt; [ $rc -eq 0 ] || exit $rc
+for l in pipe split pipesplit; do
+  SDRHIP_LIB=$PWD/ab/$l.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q \
+    -p no:cacheprovider --timeout 120 --timeout-method thread -k "resample or cfg3" > $OUT/pytest_$l.log 2>&1; rc=$?
+  tail -1 $OUT/pytest_$l.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_$l.log | head; exit $rc; }
+done
+ARMS="tree ab/pipe.so ab/split.so ab/pipesplit.so" CFGS="cfg3" REPS=3 bash scripts/ab_libs.sh > $OUT/ab_pipe.txt 2>&1; rc=$?; cat $OUT/ab_pipe.txt; [ $rc -eq 0 ] || exit $rc
 SDRHIP_LIB=$PWD/ab/pk.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q \
   -p no:cacheprovider --timeout 120 --timeout-method thread -k "u8 or odd_shapes or batched" > $OUT/pytest_pk.log 2>&1; rc=$?
 tail -2 $OUT/pytest_pk.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_pk.log | head; exit $rc; }
 ARMS="tree ab/pk.so" CFGS="cfg2u8 mono0" REPS=3 bash scripts/ab_libs.sh > $OUT/ab_pk.txt 2>&1; rc=$?; cat $OUT/ab_pk.txt; [ $rc -eq 0 ] || exit $rc
-TAG=r05b CFGS="cfg2u8 cfg3" bash scripts/prof_cfg.sh || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q \
+  -p no:cacheprovider --timeout 120 --timeout-method thread -k "f16 or cfg5" > $OUT/pytest_f16plan.log 2>&1; rc=$?
+tail -2 $OUT/pytest_f16plan.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_f16plan.log | head; exit $rc; }
+ARMS="tree:SDR_BENCH_F16_PLAN=1 tree:SDR_BENCH_F16_PLAN=0" CFGS="cfg5h" REPS=3 bash scripts/ab_libs.sh > $OUT/ab_f16plan.txt 2>&1; rc=$?
+cat $OUT/ab_f16plan.txt; [ $rc -eq 0 ] || exit $rc
+TAG=r05b CFGS="cfg2u8 cfg3 cfg5h" bash scripts/prof_cfg.sh || exit 1
 export TMPDIR=/tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_cfg2u8_$ctr" -o pmc \

@@ -346,6 +346,39 @@ def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, kswitch, kernel):
 
 
 @pytest.mark.parametrize("waves", ["8", "4"])
+@pytest.mark.parametrize("ntaps,n,ns", [(1024, 65536, 1023), (64, 4096, 63), (4096, 20000, 4095), (8, 704, 7),
+                                        (1024, 20000, 5000), (256, 8200, 255)])
+def test_fir_block_f16_plan_equals_per_call(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, ns, waves):
+    """sdr_fir_f16_plan (the MFMA kernel's tap copies built once) against the
+    per-call path that builds them in every workgroup: the same MFMA operands
+    in the same order, so outputs and the carried fp16 state are BITWISE
+    equal, two streams x two blocks; the per-call path itself is pinned to the
+    fp32 reference by the tolerance tests above."""
+    kswitch("SDR_F16_MFMA", 1)
+    kswitch("SDR_F16_W8", 1 if waves == "8" else 0)
+    sdrhip = built_lib
+    rng = np.random.default_rng(ntaps + 7 * n)
+    h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
+    S = 2
+    A = sdrhip.DeviceArray
+    d_h = A.from_numpy(gpu_ctx, h)
+    st0 = rng.standard_normal((S, ns)).astype(np.float16)
+    sth = {k: A.from_numpy(gpu_ctx, st0.reshape(-1)) for k in ("call", "plan")}
+    y = {k: A(gpu_ctx, S * n * 4) for k in ("call", "plan")}
+    plan = gpu_ctx.fir_f16_plan(d_h, ntaps)
+    try:
+        for blk in range(2):
+            xh = A.from_numpy(gpu_ctx, rng.standard_normal((S, n)).astype(np.float16))
+            gpu_ctx.fir_block_f16_dev(xh, n, S, n, d_h, ntaps, sth["call"], ns, y["call"], n)
+            plan.fir_block_f16_dev(xh, n, S, n, sth["plan"], ns, y["plan"], n)
+            gpu_ctx.synchronize()
+            assert_bits(y["plan"].download(), y["call"].download(), f"block {blk} outputs")
+            assert np.array_equal(sth["plan"].download(np.uint16), sth["call"].download(np.uint16)), "fp16 state"
+    finally:
+        plan.close()
+
+
+@pytest.mark.parametrize("waves", ["8", "4"])
 @pytest.mark.parametrize("head", ["1", "0"])
 @pytest.mark.parametrize("ns", [1500, 5000])
 def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, kswitch, ns, head, waves):
