@@ -336,6 +336,10 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // the default: cfg5h 0.0161-0.0163 vs 0.0427-0.0428 ms on the dot2 kernel
 // (profiles/r04e/ab.txt); switch SDR_F16_MFMA=0 selects v_dot2
 constexpr int kMfOut = 8192;                  // outputs per workgroup: 8 tiles of 1,024
+// SDR_F16_NT_OUT: the fp16 MFMA kernel's output stores non-temporal (A/B)
+#ifndef SDR_F16_NT_OUT
+#define SDR_F16_NT_OUT 0
+#endif
 
 struct MfArgs {
   const _Float16* x;
@@ -533,7 +537,12 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
       const float4 v = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
       if (SDR_ABL(a.ablate) == 4 && v.x != -0x1.234p100f) continue;  // (ablation 4: no stores)
       if (m + 4 <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
+#if SDR_F16_NT_OUT
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(ys + m));
+#else
         *reinterpret_cast<float4*>(ys + m) = v;
+#endif
       } else {
         const float w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

@@ -68,6 +68,10 @@
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
+// SDR_FIR_BUF: interior tiles' span loads as raw buffer loads (A/B)
+#ifndef SDR_FIR_BUF
+#define SDR_FIR_BUF 0
+#endif
 // SDR_U8_PK: fir_tile_sc's wire-byte unpack with packed FMAs (A/B)
 #ifndef SDR_U8_PK
 #define SDR_U8_PK 0
@@ -256,6 +260,47 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
       a0.y = __uint_as_float(b.y);
     }
   };
+#if SDR_FIR_BUF
+  if constexpr (!CLAMP) {
+    // interior span: raw buffer loads off a per-tile SGPR descriptor, a 32-bit
+    // lane offset and an SGPR row offset -- no 64-bit VALU address per load
+    constexpr int kAux = SRC == Src::F32 ? (SDR_FIR_NT ? 2 : 0) : (SDR_FIR_NT_U8 ? 2 : 0);  // 2: nt
+    constexpr int EB = SRC == Src::F32 ? 16 : 8;  // bytes per chunk
+    auto rsrc = [&](const void* base) __attribute__((always_inline)) {
+      return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, G::LDS4 * EB, 0x00020000);
+    };
+    auto ld = [&](int i, V& a0, V& a1, auto r0, auto r1) __attribute__((always_inline)) {
+      const int vo = EB * (i % G::NTH), so = EB * (i - i % G::NTH);
+      if constexpr (SRC == Src::F32) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v x = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r0, vo, so, kAux));
+        a0 = make_float4(x.x, x.y, x.z, x.w);
+        if (NCH == 2) {
+          const f4v y = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r1, vo, so, kAux));
+          a1 = make_float4(y.x, y.y, y.z, y.w);
+        }
+      } else {
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        const u2v b = __builtin_amdgcn_raw_buffer_load_b64(r0, vo, so, kAux);
+        a0.x = __uint_as_float(b.x);
+        a0.y = __uint_as_float(b.y);
+      }
+    };
+    if constexpr (SRC == Src::F32) {
+      const auto r0 = rsrc(tr.x0 + tr.pb);
+      const auto r1 = rsrc(NCH == 2 ? tr.x1 + tr.pb : tr.x0 + tr.pb);
+#pragma unroll
+      for (int it = 0; it < G::FULL; ++it) ld(tid + it * G::NTH, v0[it], v1[it], r0, r1);
+      if (G::REM) ld(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL], r0, r1);
+    } else {
+      const auto r0 = rsrc(tr.iq + 2 * tr.pb);
+#pragma unroll
+      for (int it = 0; it < G::FULL; ++it) ld(tid + it * G::NTH, v0[it], v1[it], r0, r0);
+      if (G::REM) ld(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL], r0, r0);
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int it = 0; it < G::FULL; ++it) load4(tid + it * G::NTH, v0[it], v1[it]);
   // ragged last row: clamp the index (a redundant load) so every register
