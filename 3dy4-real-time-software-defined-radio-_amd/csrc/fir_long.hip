@@ -336,10 +336,14 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // the default: cfg5h 0.0161-0.0163 vs 0.0427-0.0428 ms on the dot2 kernel
 // (profiles/r04e/ab.txt); switch SDR_F16_MFMA=0 selects v_dot2
 constexpr int kMfOut = 8192;                  // outputs per workgroup: 8 tiles of 1,024
-// SDR_F16_NT_OUT: the fp16 MFMA kernel's output stores non-temporal (A/B)
-#ifndef SDR_F16_NT_OUT
-#define SDR_F16_NT_OUT 0
+// SDR_F16_TSTORE: the fp16 MFMA kernel's outputs transposed through LDS so
+// each store instruction writes 1 KB contiguous (A/B)
+#ifndef SDR_F16_TSTORE
+#define SDR_F16_TSTORE 0
 #endif
+constexpr int kMfOstRow = 36;  // floats per 32-output row of a transpose area (bank spread)
+// (Round 5: the output stores non-temporal measured 0.0095 vs 0.0079 ms on
+// cfg5h, profiles/r05c/ab_f16nt.txt; not kept.)
 
 struct MfArgs {
   const _Float16* x;
@@ -356,6 +360,7 @@ struct MfArgs {
                           // 3 = no tap staging, 4 = no output stores
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
   const _Float16* hplan;  // PLAN: the 8 tap copies (8 * lc halves) prebuilt by sdr_fir_f16_plan_create
+  int ost;                // SDR_F16_TSTORE: LDS half offset of the per-wave output transpose areas
 };
 
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
@@ -529,20 +534,41 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   }
   // ---- outputs: lane (column j = i, half hh) holds rows (r & 3) + 8 (r >> 2) + 4 hh
   float* ys = a.y + (long long)s * a.y_stride;
+#if SDR_F16_TSTORE
+  float* ost = reinterpret_cast<float*>(mf_lds + a.ost) + wave * 32 * kMfOstRow;
+  const bool ys_al = (reinterpret_cast<uintptr_t>(ys) & 15) == 0;
+#endif
 #pragma unroll
   for (int t = 0; t < kMfNT; ++t) {
+#if SDR_F16_TSTORE
+    // a whole tile inside the block: through this wave's LDS area, then 4
+    // stores of 1 KB contiguous each (instead of 32 rows x 32 B per store)
+    const long long mt = m0 + tb0 + t * 1024;
+    if (ys_al && mt + 1024 <= a.n) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(ost + kMfOstRow * i + 8 * g + 4 * hh) =
+            make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = 4 * (lane + 64 * k);
+        const float4 v = *reinterpret_cast<const float4*>(ost + kMfOstRow * (q >> 5) + (q & 31));
+        *reinterpret_cast<float4*>(ys + mt + q) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the area is reused by the next tile
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
+#endif
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const long long m = m0 + tb0 + t * 1024 + 32 * i + 8 * g + 4 * hh;
       const float4 v = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
       if (SDR_ABL(a.ablate) == 4 && v.x != -0x1.234p100f) continue;  // (ablation 4: no stores)
       if (m + 4 <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
-#if SDR_F16_NT_OUT
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(ys + m));
-#else
         *reinterpret_cast<float4*>(ys + m) = v;
-#endif
       } else {
         const float w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -641,9 +667,12 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     const int head_pre = sw(kSwF16Head);  // (switch: the tests run both orders)
     a.head_pre = head_pre;
     a.hplan = static_cast<const _Float16*>(plan);
-    // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves)
-    const size_t lds = ((size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40)) *
-                       sizeof(_Float16);
+    // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves),
+    // (SDR_F16_TSTORE) one output transpose area per wave
+    const size_t taps_end = (size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40);
+    a.ost = (int)((taps_end + 7) / 8 * 8);
+    const size_t lds = (SDR_F16_TSTORE ? (size_t)a.ost * sizeof(_Float16) + 8 * 32 * kMfOstRow * sizeof(float)
+                                       : taps_end * sizeof(_Float16));
     const long long blocks = (long long)a.wg_per_stream * nstreams;
     if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
     // one launch: each stream's first workgroup commits the state itself

@@ -68,14 +68,17 @@
 #ifndef SDR_FIR_NT_U8
 #define SDR_FIR_NT_U8 0
 #endif
-// SDR_FIR_BUF: interior tiles' span loads as raw buffer loads (A/B)
+// SDR_FIR_BUF: the u8 wire path's interior span loads as raw buffer loads off
+// a per-tile SGPR descriptor (one 32-bit lane offset, SGPR row offsets) instead
+// of 64-bit per-load VALU addresses: cfg2u8 0.0764-0.0771 vs 0.0781-0.0799 ms,
+// mono0 0.0836-0.0841 vs 0.0850-0.0857 (same box, profiles/r05c/ab_buf.txt).
+// The f32 path measured 1.5 % slower that way (0.0978-0.1001 vs 0.0963-0.0977
+// ms on cfg2) and keeps its global loads.
 #ifndef SDR_FIR_BUF
-#define SDR_FIR_BUF 0
+#define SDR_FIR_BUF 1
 #endif
-// SDR_U8_PK: fir_tile_sc's wire-byte unpack with packed FMAs (A/B)
-#ifndef SDR_U8_PK
-#define SDR_U8_PK 0
-#endif
+// (Round 5: the wire-byte unpack with packed FMAs, v_pk_fma_f32 for two
+// samples, measured neutral on cfg2u8 and -1.5 % on mono0; code at 821f6db.)
 // SDR_SCAN_VCONST (timing builds only, wrong outputs): fir_tile_sc's scan
 // with a VGPR in place of the SGPR taps
 #ifndef SDR_SCAN_VCONST
@@ -261,7 +264,7 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
     }
   };
 #if SDR_FIR_BUF
-  if constexpr (!CLAMP) {
+  if constexpr (!CLAMP && SRC == Src::U8) {
     // interior span: raw buffer loads off a per-tile SGPR descriptor, a 32-bit
     // lane offset and an SGPR row offset -- no 64-bit VALU address per load
     constexpr int kAux = SRC == Src::F32 ? (SDR_FIR_NT ? 2 : 0) : (SDR_FIR_NT_U8 ? 2 : 0);  // 2: nt
@@ -1250,19 +1253,12 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     // per chunk; the second read hits L2) and unpack their own channel
     auto put = [&](int i, const float4& w) __attribute__((always_inline)) {
       const uint32_t bx = __float_as_uint(w.x), by = __float_as_uint(w.y);
-#if SDR_U8_PK
-      // two samples per packed FMA (v_pk_fma_f32): 6 instead of 8 per chunk
-      const f32x2 x01 = c == 0 ? u8_bytes_to_f32x2<0, 2>(bx) : u8_bytes_to_f32x2<1, 3>(bx);
-      const f32x2 x23 = c == 0 ? u8_bytes_to_f32x2<0, 2>(by) : u8_bytes_to_f32x2<1, 3>(by);
-      *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(x01.x, x01.y, x23.x, x23.y);
-#else
       if (c == 0)
         *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(u8_byte_to_f32<0>(bx), u8_byte_to_f32<2>(bx),
                                                               u8_byte_to_f32<0>(by), u8_byte_to_f32<2>(by));
       else
         *reinterpret_cast<float4*>(lds + 4 * i) = make_float4(u8_byte_to_f32<1>(bx), u8_byte_to_f32<3>(bx),
                                                               u8_byte_to_f32<1>(by), u8_byte_to_f32<3>(by));
-#endif
     };
 #pragma unroll
     for (int it = 0; it < G::FULL; ++it) put(lane + it * NTH, v[it]);

@@ -322,15 +322,10 @@ __global__ __launch_bounds__(kWG) void build_shifted(const float* __restrict__ h
 #ifndef SDR_LP_NT
 #define SDR_LP_NT 0
 #endif
-// SDR_LP_PIPE: the scan software-pipelined by one tap
-#ifndef SDR_LP_PIPE
-#define SDR_LP_PIPE 0
-#endif
-// SDR_LP_SPLIT: the loader wave and the compute wave on its SIMD share the
-// next item's DMA issue
-#ifndef SDR_LP_SPLIT
-#define SDR_LP_SPLIT 0
-#endif
+// Round 5 (code at 821f6db): the scan software-pipelined by
+// one tap (each add 2K-1 instructions after its multiply) measured 0.1203-
+// 0.1226 vs 0.1172-0.1189 ms, and the next item's DMAs split between the
+// loader and the compute wave on its SIMD 0.143-0.145 ms: neither kept.
 constexpr int kLpWaves = 7;
 constexpr int kLpSlots = 64 * kLpWaves;
 constexpr int kLpGroups = kLpSlots / 16;
@@ -445,7 +440,7 @@ __global__ __launch_bounds__(kLpSlots) void build_lp_tables(const float* __restr
 // or past the end.
 // The staging threads: tid of nth, in waves wv of nwv (all of the compute
 // waves, or the one loader wave).
-template <int CMAX, bool DMA_FIRST = false, bool EDGES = true>
+template <int CMAX, bool DMA_FIRST = false>
 __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, int tid, int nth, int wv, int nwv,
                                          int ln) {
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
@@ -485,16 +480,14 @@ __device__ __forceinline__ void lp_stage(const LpArgs& a, float* buf, int it, in
   // but no longer hold back their issue by a memory latency on every
   // stream's first item
   if constexpr (DMA_FIRST) dma();
-  if constexpr (EDGES) {
-    for (int j = tid; j < (int)jlo && j < nch; j += nth) edge(j);
-    for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += nth) edge(j);
-  }
+  for (int j = tid; j < (int)jlo && j < nch; j += nth) edge(j);
+  for (int j = (int)(jhi > jlo ? jhi : jlo) + tid; j < nch; j += nth) edge(j);
   if constexpr (!DMA_FIRST) dma();
 }
 
 template <int CMAX, int K, int LW, int NOLDS = 0>
 __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, int it, const float (&tp)[(CMAX + 6) / 4 * 4],
-                                           int phi, int sub, int A, int ctop0, bool valid, bool drain) {
+                                           int phi, int sub, int A, int ctop0, bool valid) {
   constexpr int NC = (CMAX + 6) / 4;
   const int st = it / a.nbat, b = it - st * a.nbat;
   const int t0 = b * a.C;
@@ -516,9 +509,6 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
   }
   float acc[K];
   f4v cur[K], nxt[K];
-#if SDR_LP_PIPE
-  float prod[K];  // the products of the previous tap, summed beside the next tap's
-#endif
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     acc[k] = 0.0f;
@@ -551,15 +541,7 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
       for (int k = 0; k < K; ++k) {
         float v = cur[k][jj];
         if (edge) v = ok ? v : 0.0f;
-#if SDR_LP_PIPE
-        // the sum of the previous tap beside the product of this one: an add
-        // never waits for the multiply just before it (2K - 1 instructions
-        // apart, across chunk ends too); same terms, same order, each rounded
-        if (cc > 0 || jj < 3) asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc[k]) : "v"(prod[k]));
-        asm volatile("v_mul_f32 %0, %1, %2" : "=v"(prod[k]) : "v"(tp[u]), "v"(v));
-#else
         acc[k] = acc[k] + tp[u] * v;
-#endif
       }
     }
 #pragma unroll
@@ -569,15 +551,10 @@ __device__ __forceinline__ void lp_compute(const LpArgs& a, const float* buf, in
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-#if SDR_LP_PIPE
-#pragma unroll
-  for (int k = 0; k < K; ++k) asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc[k]) : "v"(prod[k]));
-#endif
   // The next item's DMAs (issued before this scan) are waited for here,
   // before the output stores: vmcnt also counts stores, so a drain after them
-  // would wait out their write latency too.  (LW: the loader wave stages;
-  // `drain`: this wave issued part of the next item's DMAs, SDR_LP_SPLIT.)
-  if (!LW || drain) dma_drain();
+  // would wait out their write latency too.  (LW: the loader wave stages.)
+  if (!LW) dma_drain();
   float* ys = a.y + (long long)st * a.y_stride;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -599,11 +576,6 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
   constexpr int base0 = -(((CMAX - 1) + 3) / 4 * 4);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   const bool loader = LW && wv == kLpWaves;  // wave-uniform
-  // SDR_LP_SPLIT: the compute wave that shares the loader's SIMD (wave 3 and
-  // wave 7 both sit on SIMD 3, the one SIMD with a single compute wave)
-  // issues every other DMA instruction of the next item: neither wave then
-  // holds more than ~34 of an item's 67 in flight (vmcnt counts 63 at most)
-  const bool helper = LW && SDR_LP_SPLIT && wv == kLpWaves - 4;
   // items: contiguous range per workgroup
   const int per = a.nitems / (int)gridDim.x, extra = a.nitems % (int)gridDim.x;
   const int i0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
@@ -614,9 +586,7 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     if (!LW)
       lp_stage<CMAX>(a, buf, it, threadIdx.x, kLpSlots, wv, kLpWaves, ln);
     else if (loader)
-      lp_stage<CMAX, SDR_LP_EARLY != 0>(a, buf, it, ln, 64, 0, SDR_LP_SPLIT ? 2 : 1, ln);
-    else if (helper)
-      lp_stage<CMAX, true, false>(a, buf, it, ln, 64, 1, 2, ln);
+      lp_stage<CMAX, SDR_LP_EARLY != 0>(a, buf, it, ln, 64, 0, 1, ln);
   };
   // the first item's DMA runs while this lane's item and taps are loaded
   stage(bufA, i0);
@@ -665,9 +635,9 @@ __global__ __launch_bounds__(kLpSlots + 64 * LW, 1) void resample_lp(LpArgs a) {
     if (!(SDR_LP_EARLY && LW) && it + 1 < i1) stage(odd ? bufA : bufB, it + 1);
     if (SDR_ABL(a.ablate) != 2 && !loader) {
       if (odd)
-        lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid, helper);
+        lp_compute<CMAX, K, LW, NOLDS>(a, bufB, it, tp, phi, sub, A, ctop0, valid);
       else
-        lp_compute<CMAX, K, LW, NOLDS>(a, bufA, it, tp, phi, sub, A, ctop0, valid, helper);
+        lp_compute<CMAX, K, LW, NOLDS>(a, bufA, it, tp, phi, sub, A, ctop0, valid);
     }
     if (!LW && commit && (int)threadIdx.x < a.ns) {
       dma_drain();

@@ -61,14 +61,6 @@ __device__ __forceinline__ float u8_byte_to_f32(uint32_t w) {
   return __builtin_fmaf((float)((w >> (8 * B)) & 0xffu), 0.0078125f, -1.0f);
 }
 
-// Bytes B0 and B1 of a packed word, the same two values: two
-// v_cvt_f32_ubyte and ONE v_pk_fma_f32 (each half rounded once, exact).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int B0, int B1>
-__device__ __forceinline__ f32x2 u8_bytes_to_f32x2(uint32_t w) {
-  const f32x2 u = {(float)((w >> (8 * B0)) & 0xffu), (float)((w >> (8 * B1)) & 0xffu)};
-  return __builtin_elementwise_fma(u, f32x2{0.0078125f, 0.0078125f}, f32x2{-1.0f, -1.0f});
-}
 
 // Compute units of the calling thread's current device, cached per device
 // (the launchers run concurrently from several host threads: the drop-in's
