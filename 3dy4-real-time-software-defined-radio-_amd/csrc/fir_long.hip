@@ -337,9 +337,10 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long_h(LongHArgs a) {
 // (profiles/r04e/ab.txt); switch SDR_F16_MFMA=0 selects v_dot2
 constexpr int kMfOut = 8192;                  // outputs per workgroup: 8 tiles of 1,024
 // SDR_F16_TSTORE: the fp16 MFMA kernel's outputs transposed through LDS so
-// each store instruction writes 1 KB contiguous (A/B)
+// each store instruction writes 1 KB contiguous instead of 32 B in each of 32
+// rows: cfg5h 0.0076 vs 0.0078 ms, 3 of 3 pairs (profiles/r05d/ab_tstore.txt)
 #ifndef SDR_F16_TSTORE
-#define SDR_F16_TSTORE 0
+#define SDR_F16_TSTORE 1
 #endif
 constexpr int kMfOstRow = 36;  // floats per 32-output row of a transpose area (bank spread)
 // (Round 5: the output stores non-temporal measured 0.0095 vs 0.0079 ms on
