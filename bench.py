@@ -106,7 +106,9 @@ def parse(argv=None):
                     help="front-end FIR arithmetic: the reference's bits (exact) or one fused multiply-add per tap "
                          "(fma, tolerance-tested)")
     ap.add_argument("--batches", type=int, default=2, help="distinct input batches the steps cycle over")
-    ap.add_argument("--graph-steps", type=int, default=10, help="steps per replayed HIP graph")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps per replayed HIP graph (0: min(--steps, 100), so the timed window is one or a few "
+                         "replays and the host's launch rate never bounds a short step)")
     ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
     ap.add_argument("--stereo-pipeline", type=int, choices=(0, 1),
                     default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "1")),
@@ -553,8 +555,9 @@ class Job:
         self.launch(warmup)
         torch.cuda.synchronize(self.dev)
         t = time.perf_counter()
+        burst = self.graph[1] if self.graph is not None else 10
         while time.perf_counter() - t < seconds:
-            self.launch(10)
+            self.launch(burst)
             torch.cuda.synchronize(self.dev)
 
     def timed(self, k: int, barrier=None):
@@ -608,7 +611,7 @@ def run_device(cfg_name, device, seed, args, barrier=None, side=True):
         job.launch(args.warmup)
         job.torch.cuda.synchronize(job.dev)
         if not args.no_graph:
-            job.capture(args.graph_steps)
+            job.capture(args.graph_steps or min(max(args.steps, 1), 100))
         job.warm(0, args.warm_seconds)
         res["ms"], res["wall"] = job.timed(args.steps, barrier)
         if args.sustain_seconds > 0:
@@ -624,7 +627,7 @@ def run_device(cfg_name, device, seed, args, barrier=None, side=True):
             job.launch(max(args.warmup, 2))
             job.torch.cuda.synchronize(job.dev)
             if not args.no_graph:
-                job.capture(args.graph_steps)
+                job.capture(args.graph_steps or min(max(args.steps, 1), 100))
             job.warm(0, args.warm_seconds)
             res["fma_ms"], _ = job.timed(args.steps)
             job.ctx.set_arith(job.sdrhip.ARITH_EXACT)
@@ -721,7 +724,16 @@ def main(argv=None):
         rank, world = plan["rank"], plan["world"]
         # CPU (gloo) group: the timing barrier and max-over-ranks only; the data
         # path has no collective at all
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo's native connect prints "[Gloo] Rank r is connected to ..." on fd 1;
+        # stdout carries exactly one JSON line, so fd 1 points at stderr meanwhile
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         try:
             r = run_device(args.config, plan["devices"][0], 1234 + 7919 * rank, args, barrier=dist.barrier,
                            side=False)
@@ -778,7 +790,8 @@ def main(argv=None):
                        "parallelism": f"{world} GPU(s) x independent streams, no data-path collective "
                                       f"({'one host thread per device' if plan['mode'] == 'threads' else 'one process per device, gloo timing barrier'})",
                        "devices_opened": distinct, "input_batches": max(1, args.batches),
-                       "launch": "direct" if args.no_graph else f"HIP graph of {args.graph_steps} steps",
+                       "launch": "direct" if args.no_graph else
+                                 f"HIP graph of {args.graph_steps or min(max(args.steps, 1), 100)} steps",
                        **({"stereo_pipeline": ("two stages on two contexts' streams (front | PLL onwards), step "
                                                "b+1's front overlapping step b's recurrence")
                            if args.stereo_pipeline else "one call per step"} if job["kind"] == "stereo_u8" else {}),
