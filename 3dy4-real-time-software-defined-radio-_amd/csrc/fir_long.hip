@@ -346,6 +346,15 @@ constexpr int kMfOstRow = 36;  // floats per 32-output row of a transpose area (
 // (Round 5: the output stores non-temporal measured 0.0095 vs 0.0079 ms on
 // cfg5h, profiles/r05c/ab_f16nt.txt; not kept.)
 
+// SDR_F16_G: k-steps per fragment group of fir_long_mfma's MFMA loop (the
+// next group's 3 G reads are issued before this group's MFMAs)
+#ifndef SDR_F16_G
+#define SDR_F16_G 3
+#endif
+constexpr int kMfG = SDR_F16_G;
+constexpr int kMfMaxKd = (4096 + 31 + 32 * kMfG - 1) / (32 * kMfG) * (32 * kMfG);  // kd at T = 4096
+static_assert((kMfMaxKd + 8 + 127) / 128 * 128 + 32 + 40 <= 4424, "reversed-tap staging covers the copies");
+
 struct MfArgs {
   const _Float16* x;
   long long n, x_stride;  // halves
@@ -362,9 +371,32 @@ struct MfArgs {
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
   const _Float16* hplan;  // PLAN: the 8 tap copies (8 * lc halves) prebuilt by sdr_fir_f16_plan_create
   int ost;                // SDR_F16_TSTORE: LDS half offset of the per-wave output transpose areas
+  unsigned long long* trace;  // timing builds (SDR_F16_TRACE): per-wave phase stamps, else null
 };
 
+// Timing builds only: wall-clock stamps (100 MHz) of each wave's phases,
+// kMfTraceW per workgroup -- [k * 8 + wave], k = 0 entry, 1 after the staging
+// barrier, 2 after the MFMA loop, 3 stores issued, 4 stores complete.
+#ifdef SDR_TIMING_BUILD
+constexpr int kMfTraceW = 40;
+#define MF_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (a.trace && lane == 0) a.trace[(long long)blockIdx.x * kMfTraceW + 8 * (k) + wave] = wall_clock64(); \
+  } while (0)
+#else
+#define MF_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 __host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
+// Output row of the MFMA's row v (a permutation of 0..31 that keeps blocks of
+// four rows, so each accumulator float4 is still 4 consecutive outputs): block
+// b = v >> 2 goes to 2 (b & 3) + (b >> 2).  Row v's taps come from copy
+// (-row-1) mod 8 at row >> 3 slots back; this order gives every lane group of
+// a ds_read_b128 (both the guide's {0-3,12-15,20-27}-style groups and 16
+// consecutive lanes) 16 distinct (row & 3, row >> 3) pairs = distinct banks.
+__host__ __device__ __forceinline__ int mf_row(int v) { return 4 * (2 * ((v >> 2) & 3) + (v >> 4)) + (v & 3); }
 
 // kMfWaves waves (4: one per SIMD, two tiles each; 8: two per SIMD, one tile each).
 // PLAN: the tap copies come prebuilt (a tap plan, sdr_fir_f16_plan_*), brought
@@ -385,11 +417,13 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   const long long pb = m0 - a.ntaps;                   // stream position of image element 0 (multiple of 8)
   const _Float16* xs = a.x + (long long)s * a.x_stride;
   const _Float16* st = a.state + (long long)s * a.ns;
+  MF_STAMP(0);
   // ---- issue every load first (image chunks, taps), then write LDS: a
   // load-then-store loop waits out one memory latency per iteration.
-  // kMfChunks covers the image at T <= 4096 (span <= 12,288 halves) and
-  // kMfTaps the reversed taps (a.lc + 40 <= 4,264 halves).
-  constexpr int kNT = 64 * kMfWaves, kMfChunks = (kMfOut + 4096) / (8 * kNT), kMfTaps = (4264 + kNT - 1) / kNT;
+  // kMfChunks covers the image at T <= 4096 (span = kMfOut + kd - 32 halves)
+  // and kMfTaps the reversed taps (a.lc + 40 <= 4,424 halves).
+  constexpr int kNT = 64 * kMfWaves, kMfChunks = (kMfOut + kMfMaxKd - 32 + 8 * kNT - 1) / (8 * kNT),
+                kMfTaps = (4424 + kNT - 1) / kNT;
   const int nchunk = a.span >> 3;
   // every register defined (clamped, in-bounds addresses: n >= 8 on this
   // path), so the array stays in VGPRs; the edge chunks are rewritten below
@@ -492,9 +526,17 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     }
     __syncthreads();
   }
+  MF_STAMP(1);
+  // Lane (i, hh) supplies A's row i with the taps of output row rho = mf_row(i)
+  // (so the MFMA's row i is output row rho): with copies lc = 32 mod 128
+  // halves apart, the 16 lanes of every ds_read_b128 lane group then read 16
+  // distinct 16-B bank slots -- conflict-free (the identity mapping at
+  // lc = 1,192 cost 8 LDS cycles per A read, SQ_LDS_BANK_CONFLICT = a third
+  // of the loop's LDS cycles, profiles/r05g/)
   const int i = lane & 31, hh = lane >> 5;
-  const int q = 7 - (i & 7);                            // (-i-1) mod 8
-  const _Float16* arow = hcp + q * a.lc + (8 * hh - i - 1 + 32 - q);  // + 16 s: A fragment of step s
+  const int rho = mf_row(i);
+  const int q = 7 - (rho & 7);                          // (-rho-1) mod 8
+  const _Float16* arow = hcp + q * a.lc + (8 * hh - rho - 1 + 32 - q);  // + 16 s: A fragment of step s
   const int tb0 = wave * kMfNT * 1024;                  // this wave's first tile, relative to m0
   f16x acc[kMfNT];
 #pragma unroll
@@ -503,7 +545,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
   // G steps per group; the next group's 3 G fragments are read while this
   // group's 2 G MFMAs run (kd is a multiple of 32 G: an even group count)
-  constexpr int G = 3;
+  constexpr int G = kMfG;
   const int ngrp = SDR_ABL(a.ablate) == 2 ? 0 : a.kd / (16 * G);  // (ablation 2: no MFMA)
   half8 av[G], bv[G][kMfNT];
   auto fetch = [&](int g0, half8 (&aa)[G], half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
@@ -533,6 +575,13 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     if (g + 2 < ngrp) fetch(g + 2, av, bv);
     mfmas(an, bn);
   }
+#ifdef SDR_TIMING_BUILD
+  if (a.trace) {  // the accumulators ready (the stamp would otherwise pass the MFMAs in flight)
+#pragma unroll
+    for (int t = 0; t < kMfNT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][15]));
+  }
+#endif
+  MF_STAMP(2);
   // ---- outputs: lane (column j = i, half hh) holds rows (r & 3) + 8 (r >> 2) + 4 hh
   float* ys = a.y + (long long)s * a.y_stride;
 #if SDR_F16_TSTORE
@@ -548,7 +597,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     if (ys_al && mt + 1024 <= a.n) {
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(ost + kMfOstRow * i + 8 * g + 4 * hh) =
+        *reinterpret_cast<float4*>(ost + kMfOstRow * i + mf_row(8 * g + 4 * hh)) =
             make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
@@ -565,7 +614,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
 #endif
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const long long m = m0 + tb0 + t * 1024 + 32 * i + 8 * g + 4 * hh;
+      const long long m = m0 + tb0 + t * 1024 + 32 * i + mf_row(8 * g + 4 * hh);
       const float4 v = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
       if (SDR_ABL(a.ablate) == 4 && v.x != -0x1.234p100f) continue;  // (ablation 4: no stores)
       if (m + 4 <= a.n && ((reinterpret_cast<uintptr_t>(ys + m) & 15) == 0)) {
@@ -578,6 +627,11 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
       }
     }
   }
+#ifdef SDR_TIMING_BUILD
+  MF_STAMP(3);
+  if (a.trace) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MF_STAMP(4);
+#endif
 }
 
 // hp2[d] = (half(h[d]), half(h[d-1])) for d = 0..T, zero past both ends and
@@ -627,9 +681,39 @@ bool fir_f16_uses_mfma(int ntaps) {
 size_t fir_long_h_pairs(int ntaps) { return (size_t)((ntaps + 1 + 31) / 32 * 32); }
 
 namespace {
-int mf_kd(int ntaps) { return (ntaps + 31 + 95) / 96 * 96; }  // an even number of 3-step groups
-int mf_lc(int ntaps) { return (mf_kd(ntaps) + 40 + 7) / 8 * 8; }
+int mf_kd(int ntaps) { return (ntaps + 31 + 32 * kMfG - 1) / (32 * kMfG) * (32 * kMfG); }  // even group count
+// halves per tap copy: >= kd + 40, and 32 mod 128 (copy q's 16-B slots then
+// sit 4q mod 16 slots apart, which with mf_row makes the A reads conflict-free)
+int mf_lc(int ntaps) { return (mf_kd(ntaps) + 40 - 32 + 127) / 128 * 128 + 32; }
 }  // namespace
+
+#ifdef SDR_TIMING_BUILD
+namespace {
+unsigned long long* g_mf_trace = nullptr;
+size_t g_mf_trace_n = 0, g_mf_trace_used = 0;
+unsigned long long* mf_trace_buffer(size_t n) {  // (not for graph capture: a timing-build probe)
+  if (n > g_mf_trace_n) {
+    if (g_mf_trace) (void)hipFree(g_mf_trace);
+    if (hipMalloc(&g_mf_trace, n * sizeof(unsigned long long)) != hipSuccess) return g_mf_trace = nullptr;
+    g_mf_trace_n = n;
+  }
+  g_mf_trace_used = n;
+  return g_mf_trace;
+}
+}  // namespace
+}  // namespace sdr
+// Timing builds only: copy the last traced fir_long_mfma launch's stamps
+// (kMfTraceW per workgroup) to host; returns the count available.
+extern "C" long long sdr_timing_f16_trace(unsigned long long* host, long long max) {
+  if (!sdr::g_mf_trace) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const long long n = (long long)sdr::g_mf_trace_used < max ? (long long)sdr::g_mf_trace_used : max;
+  if (host && n > 0 && hipMemcpy(host, sdr::g_mf_trace, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return (long long)sdr::g_mf_trace_used;
+}
+namespace sdr {
+#endif
 
 size_t fir_f16_plan_halves(int ntaps) {
   return (ntaps % 8 == 0 && ntaps >= 8 && ntaps <= 4096) ? (size_t)8 * mf_lc(ntaps) : 0;
@@ -668,6 +752,11 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     const int head_pre = sw(kSwF16Head);  // (switch: the tests run both orders)
     a.head_pre = head_pre;
     a.hplan = static_cast<const _Float16*>(plan);
+    a.trace = nullptr;
+#ifdef SDR_TIMING_BUILD
+    static const int tr = SDR_TIMING_ENV("SDR_F16_TRACE", 0);
+    if (tr) a.trace = mf_trace_buffer((size_t)a.wg_per_stream * nstreams * kMfTraceW);
+#endif
     // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves),
     // (SDR_F16_TSTORE) one output transpose area per wave
     const size_t taps_end = (size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40);

@@ -272,8 +272,9 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
     auto rsrc = [&](const void* base) __attribute__((always_inline)) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, G::LDS4 * EB, 0x00020000);
     };
-    auto ld = [&](int i, V& a0, V& a1, auto r0, auto r1) __attribute__((always_inline)) {
-      const int vo = EB * (i % G::NTH), so = EB * (i - i % G::NTH);
+    // row `row` (wave-uniform: the SGPR offset), lane chunk `col`
+    auto ld = [&](int row, int col, V& a0, V& a1, auto r0, auto r1) __attribute__((always_inline)) {
+      const int vo = EB * col, so = EB * G::NTH * row;
       if constexpr (SRC == Src::F32) {
         typedef float f4v __attribute__((ext_vector_type(4)));
         const f4v x = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r0, vo, so, kAux));
@@ -293,13 +294,15 @@ __device__ __forceinline__ void stage_load_impl(const TileRef& tr, long long n, 
       const auto r0 = rsrc(tr.x0 + tr.pb);
       const auto r1 = rsrc(NCH == 2 ? tr.x1 + tr.pb : tr.x0 + tr.pb);
 #pragma unroll
-      for (int it = 0; it < G::FULL; ++it) ld(tid + it * G::NTH, v0[it], v1[it], r0, r1);
-      if (G::REM) ld(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL], r0, r1);
+      for (int it = 0; it < G::FULL; ++it) ld(it, tid, v0[it], v1[it], r0, r1);
+      // ragged last row: lanes past REM re-load its last chunk (the row offset
+      // stays uniform -- a lane-dependent one is a readfirstlane loop)
+      if (G::REM) ld(G::FULL, tid < G::REM ? tid : G::REM - 1, v0[G::FULL], v1[G::FULL], r0, r1);
     } else {
       const auto r0 = rsrc(tr.iq + 2 * tr.pb);
 #pragma unroll
-      for (int it = 0; it < G::FULL; ++it) ld(tid + it * G::NTH, v0[it], v1[it], r0, r0);
-      if (G::REM) ld(tid < G::REM ? tid + G::FULL * G::NTH : G::FULL * G::NTH - 1, v0[G::FULL], v1[G::FULL], r0, r0);
+      for (int it = 0; it < G::FULL; ++it) ld(it, tid, v0[it], v1[it], r0, r0);
+      if (G::REM) ld(G::FULL, tid < G::REM ? tid : G::REM - 1, v0[G::FULL], v1[G::FULL], r0, r0);
     }
     return;
   }

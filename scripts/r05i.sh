@@ -1,0 +1,13 @@
+#!/bin/bash
+# r05i: fir_long_mfma fragment-group size (SDR_F16_G 2/4/6 vs 3) and the
+# 4-wave shape under conflict-free A reads; f16 parity under each build.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r05i; mkdir -p $OUT
+for l in g2 g4 g6; do
+  SDRHIP_LIB=$PWD/ab/$l.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q \
+    -p no:cacheprovider --timeout 120 --timeout-method thread -k "f16 or cfg5h" > $OUT/pytest_$l.log 2>&1; rc=$?
+  echo "$l: $(tail -1 $OUT/pytest_$l.log)"; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_$l.log | head; exit $rc; }
+done
+ARMS="tree ab/g2.so ab/g4.so ab/g6.so tree:SDR_F16_W8=0" CFGS="cfg5h" REPS=3 bash scripts/ab_libs.sh > $OUT/ab_g.txt 2>&1; rc=$?; cat $OUT/ab_g.txt; [ $rc -eq 0 ] || exit $rc
+exit 0

@@ -226,3 +226,25 @@ def test_scratch_growth_refused_then_recovered(built_lib, oracle):
             assert np.array_equal(st_big, st_ref)
             small = big  # the next round must grow past the new size again
             big = rng.standard_normal(len(big) * 3).astype(np.float32)
+
+
+def test_u8_unpack_is_the_reference_conversion_for_every_byte():
+    """The u8 kernels unpack byte u as fma(float(u), 2^-7, -1) (v_cvt_f32_ubyte<k>
+    + one v_fma_f32, csrc/sdr_common.hpp u8_byte_to_f32); the reference converts
+    float(((unsigned char)u - 128) / 128.0) (src/iofunc.cpp:118).  The fma's
+    exact result u/128 - 1 is a multiple of 2^-7 in [-1, 1) -- exactly
+    representable in f32 -- so its one rounding is the identity and both give
+    the same float; for u = 128 the exact sum of +1 and -1 rounds to +0.0, the
+    reference's 0/128.0.  Checked over all 256 bytes, sign of zero included."""
+    from fractions import Fraction
+    u = np.arange(256, dtype=np.int64)
+    ref = ((u - 128) / 128.0).astype(np.float32)  # int subtract, double divide, float
+    for b in range(256):
+        exact = Fraction(b, 128) - 1  # what the fma computes before rounding
+        as_f32 = np.float32(float(exact))
+        assert Fraction(float(as_f32)) == exact  # representable: rounding is the identity
+        assert as_f32.tobytes() == ref[b].tobytes()
+    assert np.signbit(ref[128]) == False and ref[128] == 0.0  # +0.0, what fma(128, 2^-7, -1) gives
+    # the other unpack (csrc/sdr_common.hpp u8_to_f32): (float)(u - 128) * 2^-7, a product by a power of two
+    alt = (u - 128).astype(np.float32) * np.float32(0.0078125)
+    assert alt.astype(np.float32).tobytes() == ref.tobytes()
