@@ -592,23 +592,44 @@ long long sdr_resample_out_len(int up, int down, long long n) {
 
 // ------------------------------------------------------ device, batched --
 
-int sdr_fir_decim_f32_dev(sdr_ctx* c, int D, const float* x, long long n, int nstreams, long long x_stride,
-                          const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
+// side: the fast kernel's side copy (FirLaunch), pcm: s16 outputs instead of
+// y -- both only where the tiled fast path runs (the mono pipeline checks
+// fir_fast_f32 first)
+static int fir_decim_dev(sdr_ctx* c, int D, const float* x, long long n, int nstreams, long long x_stride,
+                         const float* h, int ntaps, float* state, int ns, float* y, long long y_stride,
+                         const sdr::FirLaunch* side = nullptr, int16_t* pcm = nullptr, long long pcm_stride = 0) {
   int rc = enter(c);
   if (rc) return rc;
   if ((rc = check_fir(c, D, n, nstreams, ntaps, ns, x, h, state))) return rc;
-  if (!y) return fail(c, SDR_EINVAL, "null output");
-  if (nstreams > 1 && (x_stride < n || y_stride < n / D)) return fail(c, SDR_EINVAL, "stream strides overlap");
+  if (!y && !pcm) return fail(c, SDR_EINVAL, "null output");
+  if (nstreams > 1 && (x_stride < n || (pcm ? pcm_stride : y_stride) < n / D))
+    return fail(c, SDR_EINVAL, "stream strides overlap");
   sdr::FirLaunch a = fir_args(n, nstreams, ntaps, D, ns);
   a.x0 = x;
   a.x_stride = x_stride;
   a.state0 = state;
   a.y0 = y;
   a.y_stride = y_stride;
+  a.pcm = pcm;
+  a.pcm_stride = pcm_stride;
+  if (side) {
+    a.side_src = side->side_src;
+    a.side_dst = side->side_dst;
+    a.side_src_stride = side->side_src_stride;
+    a.side_dst_stride = side->side_dst_stride;
+    a.side_n = side->side_n;
+  }
   const bool fast = vec_ok(x, x_stride, 4, nstreams);  // output alignment is handled in-kernel
+  if ((pcm || a.side_n > 0) && !(fast && sdr::fir_has_fast_path(D, ntaps, ns, 1, false, sdr::Src::F32)))
+    return fail(c, SDR_EINVAL, "internal: fused FIR outputs need the tiled fast path");
   hipError_t e = sdr::launch_fir(a, h, false, 1, sdr::Src::F32, c->cur, nullptr, nullptr, fast);
   if (e != hipSuccess) return hip_fail(c, e, "fir_decim launch");
   return SDR_OK;
+}
+
+int sdr_fir_decim_f32_dev(sdr_ctx* c, int D, const float* x, long long n, int nstreams, long long x_stride,
+                          const float* h, int ntaps, float* state, int ns, float* y, long long y_stride) {
+  return fir_decim_dev(c, D, x, n, nstreams, x_stride, h, ntaps, state, ns, y, y_stride);
 }
 
 int sdr_fir_block_f32_dev(sdr_ctx* c, const float* x, long long n, int nstreams, long long x_stride, const float* h,
@@ -630,7 +651,8 @@ int sdr_fm_demod_f32_dev(sdr_ctx* c, const float* I, const float* Q, long long n
 
 static int frontend_dev(sdr_ctx* c, sdr::Src src, int D, const float* I, const float* Q, const uint8_t* iq,
                         long long n, int nstreams, long long x_stride, const float* h, int ntaps, float* state_i,
-                        float* state_q, int ns, float* prev_i, float* prev_q, float* demod, long long out_stride) {
+                        float* state_q, int ns, float* prev_i, float* prev_q, float* demod, long long out_stride,
+                        const sdr::FirLaunch* side = nullptr) {
   int rc = enter(c);
   if (rc) return rc;
   const void* xin = src == sdr::Src::F32 ? (const void*)I : (const void*)iq;
@@ -657,6 +679,15 @@ static int frontend_dev(sdr_ctx* c, sdr::Src src, int D, const float* I, const f
     fast = vec_ok(I, x_stride, 4, nstreams) && vec_ok(Q, x_stride, 4, nstreams);
   else
     fast = vec_ok(iq, x_stride, 1, nstreams, 8);  // 8-B (4-pair) loads
+  if (side) {  // (the mono pipeline's delay line: fast path only, checked by the caller)
+    if (!(fast && sdr::fir_has_fast_path(D, ntaps, ns, 2, true, src)))
+      return fail(c, SDR_EINVAL, "internal: the front end's side copy needs the tiled fast path");
+    a.side_src = side->side_src;
+    a.side_dst = side->side_dst;
+    a.side_src_stride = side->side_src_stride;
+    a.side_dst_stride = side->side_dst_stride;
+    a.side_n = side->side_n;
+  }
   float* y0 = nullptr;
   float* y1 = nullptr;
   if (!fast || !sdr::fir_has_fast_path(D, ntaps, ns, 2, true, src)) {
@@ -956,6 +987,44 @@ int sdr_mono_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
   const long long na = sdr_resample_out_len(up, down, nd);
   if (na <= 0) return fail(c, SDR_EINVAL, "empty audio block");
   if (nstreams > 1 && pcm_stride < na) return fail(c, SDR_EINVAL, "pcm stride < audio samples per block");
+  // Fused (the tiled kernels on both filters, up == 1 -- mode 0's audio
+  // stage is FIR + decimate): one row buffer [delay state | demod] per
+  // stream.  The front end writes its output at row offset ns_delay, and its
+  // tile-0 workgroups copy the carried delay state into the row's head (their
+  // side copy), so the row's first nd floats ARE delayBlock's output
+  // (src/filter.cpp:230-238, src/project.cpp:114).  The audio FIR reads them
+  // in place, copies the row's last ns_delay floats (the new delay state) out
+  // as its side copy and stores s16 PCM itself (src/project.cpp:311-314): no
+  // delay or PCM launch, no delayed copy of the block.
+  const bool fuse_ok = up == 1 && iq && h_rf && h_audio && delay_state && state_audio && pcm && ns_delay >= 0 &&
+                       ns_delay <= 256 && nd >= ns_delay && nd % down == 0 &&
+                       vec_ok(iq, iq_stride, 1, nstreams, 8) &&
+                       sdr::fir_has_fast_path(D, rf_taps, ns_rf, 2, true, sdr::Src::U8) &&
+                       sdr::fir_has_fast_path(down, audio_taps, ns_audio, 1, false, sdr::Src::F32);
+  if (fuse_ok) {
+    const long long rstride = (ns_delay + nd + 3) / 4 * 4;  // 16-B rows: the audio FIR's fast path reads them
+    float* row = static_cast<float*>(scratch(c, kPipe0, (size_t)nstreams * rstride * sizeof(float)));
+    if (!row) return scratch_fail(c, "pipeline buffer");
+    sdr::FirLaunch head;
+    std::memset(&head, 0, sizeof head);
+    head.side_src = delay_state;
+    head.side_src_stride = ns_delay;
+    head.side_dst = row;
+    head.side_dst_stride = rstride;
+    head.side_n = ns_delay;
+    if ((rc = frontend_dev(c, sdr::Src::U8, D, nullptr, nullptr, iq, npairs, nstreams, iq_stride, h_rf, rf_taps,
+                           state_i, state_q, ns_rf, prev_i, prev_q, row + ns_delay, rstride, &head)))
+      return rc;
+    sdr::FirLaunch tail;
+    std::memset(&tail, 0, sizeof tail);
+    tail.side_src = row + nd;
+    tail.side_src_stride = rstride;
+    tail.side_dst = delay_state;
+    tail.side_dst_stride = ns_delay;
+    tail.side_n = ns_delay;
+    return fir_decim_dev(c, down, row, nd, nstreams, rstride, h_audio, audio_taps, state_audio, ns_audio, nullptr, 0,
+                         &tail, pcm, nstreams > 1 ? pcm_stride : na);
+  }
   // rows of the intermediate buffers: multiples of 4 floats (16-B aligned rows for the tiled kernels)
   const long long dstride = (nd + 3) / 4 * 4, astride = (na + 3) / 4 * 4;
   float* demod = static_cast<float*>(scratch(c, kPipe0, (size_t)nstreams * dstride * sizeof(float)));

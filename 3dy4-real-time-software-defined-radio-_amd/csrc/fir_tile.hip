@@ -158,6 +158,16 @@ __device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp)
   return (a - b) / env;
 }
 
+// FirLaunch's side copy for stream s, by the stream's tile-0 workgroup
+// (threads tid of nth): plain loads and stores, issued before that tile's
+// state-carry loads so the s_waitcnt(0) there retires them too.
+__device__ __forceinline__ void side_copy(const FirLaunch& a, int s, int tid, int nth) {
+  if (a.side_n <= 0) return;  // launch-uniform
+  const float* src = a.side_src + (long long)s * a.side_src_stride;
+  float* dst = a.side_dst + (long long)s * a.side_dst_stride;
+  for (int j = tid; j < a.side_n; j += nth) dst[j] = src[j];
+}
+
 // Input sample p (>= 0) of channel c of one stream.
 template <Src SRC>
 __device__ __forceinline__ float in_at(const float* x, const uint8_t* iq, int c, long long p) {
@@ -853,9 +863,31 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
   // its stores' write latency on top of its loads'.
   float pend[R];
   float* pend_row = nullptr;
+  int16_t* pend_pcm = nullptr;  // FIR-only launches with a.pcm: the s16 row
   long long pend_m0 = nout;  // nout: nothing pending in this lane
   bool pend_vec = false;
   auto flush = [&]() __attribute__((always_inline)) {
+    if constexpr (!DEMOD) {
+      if (a.pcm) {  // launch-uniform: s16 PCM (src/project.cpp:311-314) instead of f32
+        int16_t* o = pend_pcm;
+        if (pend_vec && pend_m0 + R <= nout) {
+          if constexpr (R == 4) {
+            typedef short s4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<s4*>(o + pend_m0) = s4{pcm_quantise(pend[0]), pcm_quantise(pend[1]),
+                                                     pcm_quantise(pend[2]), pcm_quantise(pend[3])};
+          } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) o[pend_m0 + r] = pcm_quantise(pend[r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (pend_m0 + r < nout) o[pend_m0 + r] = pcm_quantise(pend[r]);
+        }
+        pend_m0 = nout;
+        return;
+      }
+    }
     float* o = pend_row;
     if (pend_vec && pend_m0 + R <= nout) {
       if constexpr (R == 2) {
@@ -1030,16 +1062,21 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) pend[r] = acc0[r];
-      pend_row = a.y0 + (long long)tr.s * a.y_stride;
       pend_m0 = m0;
+      if (a.pcm) pend_pcm = a.pcm + (long long)tr.s * a.pcm_stride;
+      else pend_row = a.y0 + (long long)tr.s * a.y_stride;
     }
-    // vector stores when the row keeps R-float groups aligned (uniform)
-    pend_vec = ((reinterpret_cast<uintptr_t>(pend_row) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
+    // vector stores when the row keeps R-element groups aligned (uniform)
+    if (!DEMOD && a.pcm)
+      pend_vec = ((reinterpret_cast<uintptr_t>(pend_pcm) + 2ull * (unsigned long long)tr.m_start) % (2u * R)) == 0;
+    else
+      pend_vec = ((reinterpret_cast<uintptr_t>(pend_row) + 4ull * (unsigned long long)tr.m_start) % (4u * R)) == 0;
     if constexpr (!SDR_FIR_DEFER) flush();
 
     // ---- 4. state carry (tile 0 only; every read of the old values
     // happened before the barriers above)
     if (tr.t == 0) {
+      side_copy(a, tr.s, tid, NTH);
       // stage the block's last STRIP inputs (old state where p < 0: the
       // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) into the
       // channel buffers, free once every lane's scan has read them
@@ -1327,6 +1364,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   }
   // state carry (tile 0): each wave its own channel, after every read of the old values
   if (tr.t == 0) {
+    if (c == 0) side_copy(a, tr.s, lane, 64);
     float* strip = lds;  // the scan is done with it
     for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
       float w[4];
@@ -1452,6 +1490,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   a.ablate = ablate;
   static const int persist_env = SDR_TIMING_ENV("SDR_FIR_PERSIST", -1);  // A/B, timing builds
   if (persist_env >= 0) persist = persist_env != 0;
+  if (a.pcm || a.side_n > 0) persist = true;  // only fir_tile_grp implements them
   if (persist) {
     // a CU's LDS (160 KiB on gfx950, read from the device), less the claim counter
     const long long kLds = (long long)device_lds_bytes() - 64;

@@ -46,6 +46,18 @@ struct FirLaunch {
   int slab;          // fir_tile_grp: tiles per slab
   int ablate;        // timing builds only (SDR_ABL): 1 = no global loads, 2 = no FIR math, 4 = one tap pass of three
   int fma;           // SDR_ARITH_FMA: fused multiply-add FIR arithmetic where a fast path implements it
+  // Side copy, done by each stream's tile-0 workgroup after its reads (the
+  // fast tile kernels only): side_n floats side_src + s*side_src_stride ->
+  // side_dst + s*side_dst_stride.  The device mono pipeline's delay line
+  // (sdr_mono_pcm_u8_dev) rides on it: 0 = none.
+  const float* side_src;
+  float* side_dst;
+  long long side_src_stride, side_dst_stride;
+  int side_n;
+  // FIR-only launches (fir_tile_grp): outputs quantised to s16 PCM
+  // (src/project.cpp:311-314) into pcm + s*pcm_stride instead of y0; null = f32
+  int16_t* pcm;
+  long long pcm_stride;
 };
 
 // Exact reference conversion of one wire byte, src/iofunc.cpp:118:

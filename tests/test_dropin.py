@@ -204,11 +204,15 @@ def test_oracle_mono_chain_equals_reference_program(oracle, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pad", [0, 3])
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
-def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode):
+def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode, pad):
     """sdr_mono_pcm_u8_dev: several independent streams x 3 blocks, u8 IQ in,
     s16 PCM out, every byte equal to the oracle chain (itself pinned to the
-    reference program above); all carried state equal too."""
+    reference program above); all carried state equal too.  pad = 0: wire
+    rows 8-B aligned -- at up == 1 the fused layout (delay line in the front
+    end's output row, PCM from the audio FIR); pad = 3: misaligned rows, the
+    generic front end and the separate delay / FIR / PCM launches."""
     sdrhip = built_lib
     from sdrhip.synth import fm_iq_u8
 
@@ -226,10 +230,11 @@ def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode):
     d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
     got = [[] for _ in range(nstreams)]
     for b in range(nblk):
-        blk = np.stack([np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
-                        for s in range(nstreams)])
-        d_iq = A.from_numpy(gpu_ctx, np.ascontiguousarray(blk))
-        gpu_ctx.mono_pcm_u8_dev(D, d_iq, npairs, nstreams, block_bytes, d_hrf, len(h_rf), si, sq, 100, pi, pq,
+        blk = np.zeros((nstreams, block_bytes + pad), np.uint8)
+        for s in range(nstreams):
+            blk[s, :block_bytes] = np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
+        d_iq = A.from_numpy(gpu_ctx, blk)
+        gpu_ctx.mono_pcm_u8_dev(D, d_iq, npairs, nstreams, block_bytes + pad, d_hrf, len(h_rf), si, sq, 100, pi, pq,
                                 sd, 50, up, down, d_ha, len(h_audio), sa, 100, d_pcm, pcm_stride)
         gpu_ctx.synchronize()
         out = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :na]
