@@ -347,7 +347,9 @@ constexpr int kMfOstRow = 36;  // floats per 32-output row of a transpose area (
 // cfg5h, profiles/r05c/ab_f16nt.txt; not kept.)
 
 // SDR_F16_G: k-steps per fragment group of fir_long_mfma's MFMA loop (the
-// next group's 3 G reads are issued before this group's MFMAs)
+// next group's 2 G reads are issued before this group's MFMAs).  3 measured
+// best: 2 / 4 / 6 gave cfg5h 0.0075-0.0077 vs 0.0071-0.0073 ms
+// (profiles/r05i/ab_g.txt)
 #ifndef SDR_F16_G
 #define SDR_F16_G 3
 #endif
