@@ -997,7 +997,7 @@ int sdr_mono_pcm_u8_dev(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, 
   // as its side copy and stores s16 PCM itself (src/project.cpp:311-314): no
   // delay or PCM launch, no delayed copy of the block.
   const bool fuse_ok = up == 1 && iq && h_rf && h_audio && delay_state && state_audio && pcm && ns_delay >= 0 &&
-                       ns_delay <= 256 && nd >= ns_delay && nd % down == 0 &&
+                       ns_delay <= 256 /* the side copy's 4 per lane of a wave */ && nd >= ns_delay && nd % down == 0 &&
                        vec_ok(iq, iq_stride, 1, nstreams, 8) &&
                        sdr::fir_has_fast_path(D, rf_taps, ns_rf, 2, true, sdr::Src::U8) &&
                        sdr::fir_has_fast_path(down, audio_taps, ns_audio, 1, false, sdr::Src::F32);

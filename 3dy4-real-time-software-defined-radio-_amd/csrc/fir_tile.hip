@@ -159,13 +159,26 @@ __device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp)
 }
 
 // FirLaunch's side copy for stream s, by the stream's tile-0 workgroup
-// (threads tid of nth): plain loads and stores, issued before that tile's
-// state-carry loads so the s_waitcnt(0) there retires them too.
-__device__ __forceinline__ void side_copy(const FirLaunch& a, int s, int tid, int nth) {
-  if (a.side_n <= 0) return;  // launch-uniform
+// (threads tid of nth, side_n <= kSideMax * nth, checked by the C API): the
+// loads go out in the same batch as that tile's state-carry loads and the
+// stores after their s_waitcnt(0) -- one memory latency for both, not two.
+constexpr int kSideMax = 4;
+__device__ __forceinline__ void side_load(const FirLaunch& a, int s, int tid, int nth, float (&v)[kSideMax]) {
   const float* src = a.side_src + (long long)s * a.side_src_stride;
+#pragma unroll
+  for (int u = 0; u < kSideMax; ++u) {
+    const int j = tid + u * nth;
+    v[u] = 0.0f;
+    if (j < a.side_n) v[u] = src[j];
+  }
+}
+__device__ __forceinline__ void side_store(const FirLaunch& a, int s, int tid, int nth, const float (&v)[kSideMax]) {
   float* dst = a.side_dst + (long long)s * a.side_dst_stride;
-  for (int j = tid; j < a.side_n; j += nth) dst[j] = src[j];
+#pragma unroll
+  for (int u = 0; u < kSideMax; ++u) {
+    const int j = tid + u * nth;
+    if (j < a.side_n) dst[j] = v[u];
+  }
 }
 
 // Input sample p (>= 0) of channel c of one stream.
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(64 * NW) void fir_tile(FirLaunch a, const float* __
     }
     if (SDR_ABL(a.ablate) == 2) {
       acc0[0] = lds0[lbase];
-      acc1[0] = lds1[lbase];
+      if (NCH == 2) acc1[0] = lds1[lbase];
     } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
@@ -777,7 +790,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // Launch shape: persistent workgroups (a group each, one or two per CU),
-// blockDim.x / 64 waves each.  Every wave owns one LDS slice of G::SMEM
+// blockDim.x / 64 waves each.  Every wave owns one LDS slice of grp_slice()
 // floats and works through the group's tiles on its own, claiming the next
 // one from a counter in LDS when its staging is done, so the waves on a
 // lightly loaded SIMD take more tiles than those sharing a SIMD with more
@@ -795,6 +808,16 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SDR_FIR_LB
 #define SDR_FIR_LB 1024
 #endif
+// fir_tile_grp's LDS floats per wave: one span per channel (a one-channel
+// FIR needs half of fir_tile's two-channel slice: 16 waves of the D = 5 / 1
+// FIRs fit a CU instead of 14, one round of tiles instead of two)
+#ifndef SDR_GRP_CH_SLICE
+#define SDR_GRP_CH_SLICE 1  // 0: two spans per wave whatever NCH (the round-4 layout, A/B)
+#endif
+template <int D, int T, int R, bool DEMOD, int NCH>
+constexpr int grp_slice() {
+  return (SDR_GRP_CH_SLICE ? NCH : 2) * Geom<D, T, R, DEMOD, 1>::LDS_LEN;
+}
 template <int D, int T, int R, int NW, int NCH, bool DEMOD, Src SRC, int TM, bool FMA = false>
 __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const float* __restrict__ h) {
   using G = Geom<D, T, R, DEMOD, NW>;
@@ -807,7 +830,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int next_tile;  // the group's claim counter
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* lds0 = smem + wv * G::SMEM;  // this wave's slice
+  float* lds0 = smem + wv * grp_slice<D, T, R, DEMOD, NCH>();  // this wave's slice
   float* lds1 = lds0 + G::LDS_LEN;
   float* strip0 = lds0;  // the block's last inputs (tile 0, after its scan)
   float* strip1 = lds1;
@@ -968,7 +991,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     }
     if (SDR_ABL(a.ablate) == 2) {
       acc0[0] = lds0[lbase];
-      acc1[0] = lds1[lbase];
+      if (NCH == 2) acc1[0] = lds1[lbase];
     } else {
       const float* w0 = lds0 + lbase;
       const float* w1 = lds1 + lbase;
@@ -1076,7 +1099,8 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     // ---- 4. state carry (tile 0 only; every read of the old values
     // happened before the barriers above)
     if (tr.t == 0) {
-      side_copy(a, tr.s, tid, NTH);
+      float side[kSideMax];
+      side_load(a, tr.s, tid, NTH, side);
       // stage the block's last STRIP inputs (old state where p < 0: the
       // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) into the
       // channel buffers, free once every lane's scan has read them
@@ -1103,6 +1127,7 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
         }
       }
       __builtin_amdgcn_s_waitcnt(0);  // as in edge_fill: keep the waitcnt pass from draining at the next scan
+      side_store(a, tr.s, tid, NTH, side);
       wave_sync();
       if constexpr (DEMOD) {
         // prev_* <- last decimated I/Q of the block (src/filter.cpp:100-101),
@@ -1364,7 +1389,8 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   }
   // state carry (tile 0): each wave its own channel, after every read of the old values
   if (tr.t == 0) {
-    if (c == 0) side_copy(a, tr.s, lane, 64);
+    float side[kSideMax];
+    if (c == 0) side_load(a, tr.s, lane, 64, side);
     float* strip = lds;  // the scan is done with it
     for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
       float w[4];
@@ -1380,6 +1406,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
       }
     }
     __builtin_amdgcn_s_waitcnt(0);
+    if (c == 0) side_store(a, tr.s, lane, 64, side);
     wave_sync();
     if (lane == 0) {
       // prev_c <- this channel's last decimated output (src/filter.cpp:100-101),
@@ -1494,7 +1521,7 @@ hipError_t run_tile(const FirLaunch& a0, const float* h, hipStream_t st, bool pe
   if (persist) {
     // a CU's LDS (160 KiB on gfx950, read from the device), less the claim counter
     const long long kLds = (long long)device_lds_bytes() - 64;
-    constexpr long long slice = (long long)G::SMEM * sizeof(float);
+    constexpr long long slice = (long long)grp_slice<D, T, R, DEMOD, NCH>() * sizeof(float);
     if (kLds < slice) return hipErrorInvalidConfiguration;
     static const int wpg_env = SDR_TIMING_ENV("SDR_FIR_WPG", 0);  // timing builds
     long long wpg = std::min<long long>(16, kLds / slice);
