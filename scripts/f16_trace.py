@@ -38,7 +38,9 @@ for r in range(50 + reps):
         cnt = L.sdr_timing_f16_trace(None, 0)
         buf = np.zeros(cnt, dtype=np.uint64)
         L.sdr_timing_f16_trace(buf.ctypes.data, cnt)
-        rows.append(buf.reshape(-1, 5, 8).astype(np.int64))
+        t = buf.reshape(-1, 5, 8).astype(np.int64)
+        nw = int((t[:, 0, :] != 0).any(axis=0).sum())  # waves per workgroup (4 or 8)
+        rows.append(t[:, :, :nw])
 for r, t in enumerate(rows):
     t0 = t[:, 0, :].min()
     rel = (t - t0) * 10e-3  # us
@@ -54,6 +56,10 @@ for r, t in enumerate(rows):
     print("  barrier time (abs)           ", q(bar))
     print("  MFMA done (abs)              ", q(mf))
     print("  done (abs)                   ", q(done))
+    stw = (bar - entry).max(axis=1)  # per workgroup: slowest wave's staging wait
+    worst = np.argsort(stw)[-6:][::-1]
+    print("  slowest staging (workgroup: us):", ", ".join(f"{w}: {stw[w]:.2f}" for w in worst),
+          "| workgroup 0:", f"{stw[0]:.2f}", "| last of stream 0:", f"{stw[t.shape[0] // 2 - 1]:.2f}")
     wg_first = t[:, 0, :].min(axis=1)
     order = np.argsort(wg_first)
     print("  last-entry workgroups:", order[-4:].tolist(), "first-entry:", order[:4].tolist())
