@@ -343,7 +343,6 @@ constexpr int kMfOut = 8192;                  // outputs per workgroup: 8 tiles 
 #define SDR_F16_TSTORE 1
 #endif
 constexpr int kMfOstRow = 36;  // floats per 32-output row of a transpose area (bank spread)
-constexpr int kMf64OstRow = 68;  // the 64-row shape: floats per 64-output column
 // (Round 5: the output stores non-temporal measured 0.0095 vs 0.0079 ms on
 // cfg5h, profiles/r05c/ab_f16nt.txt; not kept.)
 
@@ -356,16 +355,7 @@ constexpr int kMf64OstRow = 68;  // the 64-row shape: floats per 64-output colum
 #endif
 constexpr int kMfG = SDR_F16_G;
 constexpr int kMfMaxKd = (4096 + 31 + 32 * kMfG - 1) / (32 * kMfG) * (32 * kMfG);  // kd at T = 4096
-// the 64-row shape (fir_long_mfma<4, PLAN, 64>): K extent T + 64 rounded to 4-step groups
-#ifndef SDR_F16_G64
-#define SDR_F16_G64 4
-#endif
-constexpr int kMf64G = SDR_F16_G64;  // k-steps per group (an even group count: kd a multiple of 32 G)
-__host__ __device__ constexpr int mf_kd64(int ntaps) { return (ntaps + 64 + 32 * kMf64G - 1) / (32 * kMf64G) * (32 * kMf64G); }
-constexpr int kMfMaxKd64 = mf_kd64(4096);
-constexpr int kMfMaxSpan = (kMfMaxKd - 32 > kMfMaxKd64 - 64 ? kMfMaxKd - 32 : kMfMaxKd64 - 64);  // + kMfOut
-constexpr int kMfMaxKdAll = kMfMaxKd > kMfMaxKd64 ? kMfMaxKd : kMfMaxKd64;
-static_assert((kMfMaxKdAll + 8 + 127) / 128 * 128 + 32 + 40 <= 4424, "reversed-tap staging covers the copies");
+static_assert((kMfMaxKd + 8 + 127) / 128 * 128 + 32 + 40 <= 4424, "reversed-tap staging covers the copies");
 
 struct MfArgs {
   const _Float16* x;
@@ -379,7 +369,7 @@ struct MfArgs {
   int wg_per_stream;
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
   int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
-                          // 3 = no tap staging, 4 = no output stores
+                          // 3 = no tap staging, 4 = no output stores, 7 = the head as interior, 8 = no head loads
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
   const _Float16* hplan;  // PLAN: the 8 tap copies (8 * lc halves) prebuilt by sdr_fir_f16_plan_create
   int ost;                // SDR_F16_TSTORE: LDS half offset of the per-wave output transpose areas
@@ -401,11 +391,7 @@ constexpr int kMfTraceW = 40;
   } while (0)
 #endif
 
-// padded LDS half index of the input image: 16 B of pad per B-column stride
-// (RW halves), so the 32 columns' 16-B fragment reads land on distinct banks
-template <int RW>
-__host__ __device__ __forceinline__ int mfpad(int p) { return p + 8 * (p >> (RW == 64 ? 6 : 5)); }
-__host__ __device__ __forceinline__ int mf_pad(int p) { return mfpad<32>(p); }
+__host__ __device__ __forceinline__ int mf_pad(int p) { return p + 8 * (p >> 5); }  // padded LDS half index
 // Output row of the MFMA's row v (a permutation of 0..31 that keeps blocks of
 // four rows, so each accumulator float4 is still 4 consecutive outputs): block
 // b = v >> 2 goes to 2 (b & 3) + (b >> 2).  Row v's taps come from copy
@@ -418,20 +404,14 @@ __host__ __device__ __forceinline__ int mf_row(int v) { return 4 * (2 * ((v >> 2
 // PLAN: the tap copies come prebuilt (a tap plan, sdr_fir_f16_plan_*), brought
 // into LDS by LDS-DMA beside the image loads -- no f32 tap loads, no reversed
 // row, no copy pass and one barrier fewer; else they are built here.
-// RW = 64 (4 waves, SDR_F16_R64): each wave owns 2,048 outputs m = tb + 64 j
-// + row, rows 0..63 as two MFMA row blocks that share every B fragment; the
-// second block's A fragment at step s is the first block's at step s - 2
-// (its taps sit 32 further along the band), already in registers -- one A
-// and one B read per TWO MFMAs instead of per one.
-template <int kMfWaves, bool PLAN = false, int RW = 32>
+template <int kMfWaves, bool PLAN = false>
 __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
-  static_assert(RW == 32 || (RW == 64 && kMfWaves == 4), "64-row tiles: four waves of 2,048 outputs");
-  constexpr int kMfNT = 8 / kMfWaves;           // 1,024-output tiles per wave (RW = 32)
+  constexpr int kMfNT = 8 / kMfWaves;           // 1,024-output tiles per wave
   typedef _Float16 half8 __attribute__((ext_vector_type(8)));
   typedef float f16x __attribute__((ext_vector_type(16)));
   extern __shared__ __attribute__((aligned(16))) _Float16 mf_lds[];
   _Float16* img = mf_lds;                              // padded input image
-  _Float16* hcp = mf_lds + mfpad<RW>(a.span) + 8;      // 8 tap copies, a.lc halves each
+  _Float16* hcp = mf_lds + mf_pad(a.span) + 8;         // 8 tap copies, a.lc halves each
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int s = blockIdx.x / a.wg_per_stream;
@@ -444,25 +424,25 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // load-then-store loop waits out one memory latency per iteration.
   // kMfChunks covers the image at T <= 4096 (span = kMfOut + kd - 32 halves)
   // and kMfTaps the reversed taps (a.lc + 40 <= 4,424 halves).
-  constexpr int kNT = 64 * kMfWaves, kMfChunks = (kMfOut + kMfMaxSpan + 8 * kNT - 1) / (8 * kNT),
+  constexpr int kNT = 64 * kMfWaves, kMfChunks = (kMfOut + kMfMaxKd - 32 + 8 * kNT - 1) / (8 * kNT),
                 kMfTaps = (4424 + kNT - 1) / kNT;
   // the stream's first workgroup (pb = -T, T <= 4096 = kMfSt * kNT): the
   // carried state for image positions q in [-T, 0) and the new state (the
   // block's last ns inputs, src/filter.cpp:82) join the same load batch, so
   // this workgroup waits out one memory latency like the others, not three.
   // Issued FIRST: they touch two pages no other workgroup does (the state
-  // buffer, the row's tail), whose translation misses cost about a memory
-  // latency more (phase trace: 2.2 vs 1.0 us of staging, profiles/r05o/)
+  // buffer, the row's tail); issued after the image loads they left these
+  // workgroups staging 2.2 vs 1.0 us (phase trace, profiles/r05o/, r05p/)
   constexpr int kMfSt = 4096 / kNT;
-  const bool head = a.head_pre && pb < 0 && SDR_ABL(a.ablate) != 7;  // (7: the head treated as interior)
+  const bool head = a.head_pre && pb < 0 && SDR_ABL(a.ablate) != 7;  // (timing 7: head as interior)
   _Float16 sv[kMfSt], nv[kMfSt];
   if (head) {
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
       const int q = (int)pb + tid + k * kNT;
-      sv[k] = (q < 0 && q >= -a.ns && SDR_ABL(a.ablate) != 5 && SDR_ABL(a.ablate) != 8) ? st[a.ns + q] : (_Float16)0;  // (5: no state loads)
+      sv[k] = (q < 0 && q >= -a.ns && SDR_ABL(a.ablate) != 8) ? st[a.ns + q] : (_Float16)0;  // (8: no head loads)
       const int i = tid + k * kNT;
-      nv[k] = (i < a.ns && SDR_ABL(a.ablate) != 6 && SDR_ABL(a.ablate) != 8) ? xs[a.n - a.ns + i] : (_Float16)0;  // (6: no new-state loads)
+      nv[k] = (i < a.ns && SDR_ABL(a.ablate) != 8) ? xs[a.n - a.ns + i] : (_Float16)0;
     }
   }
   const int nchunk = a.span >> 3;
@@ -498,13 +478,13 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
 #pragma unroll
   for (int k = 0; k < kMfChunks; ++k) {
     const int c = tid + k * kNT;
-    if (c < nchunk && !(head && pb + 8LL * c < 0)) *reinterpret_cast<u32x4*>(img + mfpad<RW>(8 * c)) = iv[k];
+    if (c < nchunk && !(head && pb + 8LL * c < 0)) *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
   }
   if (head) {
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
       const int q = (int)pb + tid + k * kNT;
-      if (q < 0) img[mfpad<RW>(q - (int)pb)] = sv[k];
+      if (q < 0 && SDR_ABL(a.ablate) != 11) img[mf_pad(q - (int)pb)] = sv[k];
     }
   }
   // block edges (the stream's first and last workgroups), element-wise over
@@ -513,7 +493,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     for (int c = tid; c < nchunk; c += kNT) {
       const long long p = pb + 8LL * c;
       if ((p >= 0 || head) && p + 8 <= a.n) continue;
-      _Float16* d = img + mfpad<RW>(8 * c);
+      _Float16* d = img + mf_pad(8 * c);
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const long long q = p + r;
@@ -532,7 +512,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // the stream's first workgroup is the only reader of the old state (staged
   // above): it writes the new one, the block's last ns inputs
   // (src/filter.cpp:82), after that barrier
-  if (head) {
+  if (head && SDR_ABL(a.ablate) != 10) {  // (timing 10: no new-state stores; 11: no state LDS writes)
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k)
       if (tid + k * kNT < a.ns) a.state[(long long)s * a.ns + tid + k * kNT] = nv[k];
@@ -562,96 +542,6 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   const int rho = mf_row(i);
   const int q = 7 - (rho & 7);                          // (-rho-1) mod 8
   const _Float16* arow = hcp + q * a.lc + (8 * hh - rho - 1 + 32 - q);  // + 16 s: A fragment of step s
-  if constexpr (RW == 64) {
-    // ---- 64-row tiles: rows 0..31 (acc1) and 32..63 (acc2) of 32 columns 64
-    // outputs apart; one A (rows 0..31) and one B read per step, two MFMAs.
-    // Groups of kMf64G steps, two register sets in ping-pong (an even group
-    // count, as in the 32-row loop: the accumulators stay put); the previous
-    // group's last two A fragments (the second block's A for this group's
-    // first two steps) are kept aside before their set is refilled.
-    constexpr int GG = kMf64G;
-    const int tb = wave * 2048;
-    f16x acc1, acc2;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc1[r] = acc2[r] = 0.0f;
-    const int ngrp = SDR_ABL(a.ablate) == 2 ? 0 : a.kd / (16 * GG);
-    half8 a0[GG], b0[GG], a1[GG], b1[GG], hist[2];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) hist[0][k] = hist[1][k] = (_Float16)0;  // A before the band: zero taps
-    auto fetch = [&](int g0, half8 (&aa)[GG], half8 (&bb)[GG]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int u = 0; u < GG; ++u) {
-        const int sidx = g0 * GG + u;
-        aa[u] = *reinterpret_cast<const half8*>(arow + 16 * sidx);
-        bb[u] = *reinterpret_cast<const half8*>(img + mfpad<64>(tb + 64 * i + 16 * sidx + 8 * hh));
-      }
-    };
-    auto mfmas = [&](const half8 (&aa)[GG], const half8 (&bb)[GG], const half8 (&hp)[2]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int u = 0; u < GG; ++u) {
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[u], bb[u], acc1, 0, 0, 0);
-        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(u >= 2 ? aa[u - 2] : hp[u], bb[u], acc2, 0, 0, 0);
-      }
-    };
-    half8 hist2[2];
-    fetch(0, a0, b0);
-    for (int g = 0; g < ngrp; g += 2) {
-      fetch(g + 1, a1, b1);  // (a1's group g - 1 fragments were kept in hist)
-      mfmas(a0, b0, hist);
-      hist2[0] = a0[GG - 2];
-      hist2[1] = a0[GG - 1];
-      if (g + 2 < ngrp) fetch(g + 2, a0, b0);
-      mfmas(a1, b1, hist2);
-      hist[0] = a1[GG - 2];
-      hist[1] = a1[GG - 1];
-    }
-#ifdef SDR_TIMING_BUILD
-    if (a.trace) asm volatile("" ::"v"(acc1[0]), "v"(acc1[15]), "v"(acc2[0]), "v"(acc2[15]));
-#endif
-    MF_STAMP(2);
-    // ---- outputs: column j = i, rows mf_row((r & 3) + 8 (r >> 2) + 4 hh) (+ 32 for acc2)
-    float* ys = a.y + (long long)s * a.y_stride;
-    const long long mt = m0 + tb;
-    float* ost = reinterpret_cast<float*>(mf_lds + a.ost) + wave * 32 * kMf64OstRow;
-    if ((reinterpret_cast<uintptr_t>(ys) & 15) == 0 && mt + 2048 <= a.n) {
-      // through this wave's LDS area (column stride 68 floats: conflict-free
-      // float4 writes), then 8 stores of 1 KB contiguous each
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int r0 = mf_row(8 * g + 4 * hh);
-        *reinterpret_cast<float4*>(ost + kMf64OstRow * i + r0) =
-            make_float4(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
-        *reinterpret_cast<float4*>(ost + kMf64OstRow * i + 32 + r0) =
-            make_float4(acc2[4 * g], acc2[4 * g + 1], acc2[4 * g + 2], acc2[4 * g + 3]);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int qq = 4 * (lane + 64 * k);
-        const float4 v = *reinterpret_cast<const float4*>(ost + kMf64OstRow * (qq >> 6) + (qq & 63));
-        *reinterpret_cast<float4*>(ys + mt + qq) = v;
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const long long m = mt + 64 * i + mf_row(8 * g + 4 * hh);
-        const float w1[4] = {acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]};
-        const float w2[4] = {acc2[4 * g], acc2[4 * g + 1], acc2[4 * g + 2], acc2[4 * g + 3]};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (m + r < a.n) ys[m + r] = w1[r];
-          if (m + 32 + r < a.n) ys[m + 32 + r] = w2[r];
-        }
-      }
-    }
-#ifdef SDR_TIMING_BUILD
-    MF_STAMP(3);
-    if (a.trace) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    MF_STAMP(4);
-#endif
-    return;
-  }
   const int tb0 = wave * kMfNT * 1024;                  // this wave's first tile, relative to m0
   f16x acc[kMfNT];
 #pragma unroll
@@ -799,10 +689,7 @@ namespace {
 int mf_kd(int ntaps) { return (ntaps + 31 + 32 * kMfG - 1) / (32 * kMfG) * (32 * kMfG); }  // even group count
 // halves per tap copy: >= kd + 40, and 32 mod 128 (copy q's 16-B slots then
 // sit 4q mod 16 slots apart, which with mf_row makes the A reads conflict-free)
-int mf_lc(int ntaps) {  // one plan layout for both tile shapes: the larger K extent
-  const int kd = mf_kd(ntaps) > mf_kd64(ntaps) ? mf_kd(ntaps) : mf_kd64(ntaps);
-  return (kd + 40 - 32 + 127) / 128 * 128 + 32;
-}
+int mf_lc(int ntaps) { return (mf_kd(ntaps) + 40 - 32 + 127) / 128 * 128 + 32; }
 }  // namespace
 
 #ifdef SDR_TIMING_BUILD
@@ -857,15 +744,14 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     a.x_stride = x_stride;
     a.h = h;
     a.ntaps = ntaps;
-    const bool r64 = sw(kSwF16R64) != 0;  // 64-row tiles (4 waves)
-    a.kd = r64 ? mf_kd64(ntaps) : mf_kd(ntaps);  // zero taps past the band
+    a.kd = mf_kd(ntaps);  // zero taps past the band
     a.lc = mf_lc(ntaps);
     a.state = static_cast<_Float16*>(state);
     a.ns = ns;
     a.y = y;
     a.y_stride = y_stride;
     a.wg_per_stream = (int)((n + kMfOut - 1) / kMfOut);
-    a.span = kMfOut + a.kd - (r64 ? 64 : 32);
+    a.span = kMfOut + a.kd - 32;
     static const int ablate = SDR_TIMING_ENV("SDR_ABLATE", 0);
     a.ablate = ablate;
     const int head_pre = sw(kSwF16Head);  // (switch: the tests run both orders)
@@ -878,23 +764,17 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
 #endif
     // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves),
     // (SDR_F16_TSTORE) one output transpose area per wave
-    const size_t taps_end = (size_t)(r64 ? mfpad<64>(a.span) : mf_pad(a.span)) + 8 + (plan ? 8 : 9) * (size_t)a.lc +
-                            (plan ? 0 : 40);
+    const size_t taps_end = (size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40);
     a.ost = (int)((taps_end + 7) / 8 * 8);
-    const size_t lds = r64 ? (size_t)a.ost * sizeof(_Float16) + 4 * 32 * kMf64OstRow * sizeof(float)
-                           : (SDR_F16_TSTORE ? (size_t)a.ost * sizeof(_Float16) + 8 * 32 * kMfOstRow * sizeof(float)
-                                             : taps_end * sizeof(_Float16));
+    const size_t lds = (SDR_F16_TSTORE ? (size_t)a.ost * sizeof(_Float16) + 8 * 32 * kMfOstRow * sizeof(float)
+                                       : taps_end * sizeof(_Float16));
     const long long blocks = (long long)a.wg_per_stream * nstreams;
     if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
     // one launch: each stream's first workgroup commits the state itself
     // two waves per SIMD, one tile each: 8.8 vs 10.9 us per kernel on cfg5h
     // (profiles/r04y/); SDR_F16_W8=0 restores four waves of two tiles
     const int w8 = sw(kSwF16W8);
-    if (r64 && plan)
-      hipLaunchKernelGGL((fir_long_mfma<4, true, 64>), dim3((unsigned)blocks), dim3(256), lds, st, a);
-    else if (r64)
-      hipLaunchKernelGGL((fir_long_mfma<4, false, 64>), dim3((unsigned)blocks), dim3(256), lds, st, a);
-    else if (w8 && plan)
+    if (w8 && plan)
       hipLaunchKernelGGL((fir_long_mfma<8, true>), dim3((unsigned)blocks), dim3(512), lds, st, a);
     else if (w8)
       hipLaunchKernelGGL((fir_long_mfma<8, false>), dim3((unsigned)blocks), dim3(512), lds, st, a);

@@ -1298,7 +1298,10 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     tr.st0 = tr.st1;
   }
   float old_pi = 0.0f, old_pq = 0.0f;
-  if (c == 0 && tr.t == 0) {
+  // (timing ablation 9: tile 0 without its extra work -- wrong outputs; how
+  // much the streams' first tiles cost the launch)
+  const bool t0x = tr.t == 0 && SDR_ABL(a.ablate) != 9;
+  if (c == 0 && t0x) {
     using cf = const __attribute__((address_space(4))) float*;
     const int s = __builtin_amdgcn_readfirstlane(tr.s);
     old_pi = ((cf)a.prev0)[s];
@@ -1329,7 +1332,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     for (int it = 0; it < G::FULL; ++it) put(lane + it * NTH, v[it]);
     if (G::REM && lane < G::REM) put(lane + G::FULL * NTH, v[G::FULL]);
   }
-  if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {
+  if (t0x || (tr.t != 0 && !interior<D, T, R, DEMOD, NW>(tr, n))) {
     wave_sync();
     edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, lane, n, ns, [&](int i, float v0, float) { lds[i] = v0; }, c);
   }
@@ -1388,7 +1391,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     }
   }
   // state carry (tile 0): each wave its own channel, after every read of the old values
-  if (tr.t == 0) {
+  if (t0x) {
     float side[kSideMax];
     if (c == 0) side_load(a, tr.s, lane, 64, side);
     float* strip = lds;  // the scan is done with it

@@ -102,7 +102,6 @@ enum Switch : int {
   kSwF16Mfma,         // SDR_F16_MFMA: fp16 arm on the MFMA Toeplitz GEMM (1) or v_dot2 (0)
   kSwF16Head,         // SDR_F16_HEAD: fir_long_mfma's first workgroup loads its state in the first batch
   kSwF16W8,           // SDR_F16_W8: fir_long_mfma as 8 waves of one tile (1) or 4 of two (0)
-  kSwF16R64,          // SDR_F16_R64: fir_long_mfma as 4 waves of 64-row tiles (wins over SDR_F16_W8)
   kSwPllFast,         // SDR_PLL_FAST: certified short-chain PLL step (1) or library routines (0)
   kSwPllGuard,        // SDR_PLL_GUARD: the PLL's chunk input checks as a parallel pre-pass
   kSwCount

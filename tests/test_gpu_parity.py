@@ -270,7 +270,7 @@ def test_resample_many_streams(gpu_ctx, oracle, built_lib, up, down, cnt, nstrea
         assert_bits(d_st.download().reshape(nstreams, ns), states, f"state block {blk}")
 
 
-@pytest.mark.parametrize("kernel", ["mfma", "mfma64", "dot2"])
+@pytest.mark.parametrize("kernel", ["mfma", "dot2"])
 @pytest.mark.parametrize("ntaps,n", [(1024, 65536), (64, 4096), (101, 5000), (1024, 3000), (256, 8200), (8, 704),
                                     (4096, 20000)])
 def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, kernel):
@@ -280,8 +280,7 @@ def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, 
     of the exact fp32 reference, and within fp32 accumulation error of the
     exact sum over the fp16-rounded operands.  The carried fp16 state is the
     last ns inputs, exactly."""
-    kswitch("SDR_F16_MFMA", "0" if kernel == "dot2" else "1")
-    kswitch("SDR_F16_R64", "1" if kernel == "mfma64" else "0")
+    kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(ntaps + n)
     h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
@@ -312,13 +311,12 @@ def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, 
                               x[:, -ns:].astype(np.float16)), "fp16 state"
 
 
-@pytest.mark.parametrize("kernel", ["mfma", "mfma64", "dot2"])
+@pytest.mark.parametrize("kernel", ["mfma", "dot2"])
 def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, kswitch, kernel):
     """The fp16 arm on padded rows (x_stride, y_stride > n) over 3 streams, two
     blocks: each stream within the tolerance of its own exact fp32 filter, the
     padding never written, the fp16 state exact."""
-    kswitch("SDR_F16_MFMA", "0" if kernel == "dot2" else "1")
-    kswitch("SDR_F16_R64", "1" if kernel == "mfma64" else "0")
+    kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(77)
     ntaps, n, nstreams = 1024, 20000, 3
@@ -347,7 +345,7 @@ def test_fir_block_f16_padded_rows(gpu_ctx, oracle, built_lib, kswitch, kernel):
                               x[:, -ns:].astype(np.float16)), "fp16 state"
 
 
-@pytest.mark.parametrize("waves", ["8", "4", "r64"])
+@pytest.mark.parametrize("waves", ["8", "4"])
 @pytest.mark.parametrize("ntaps,n,ns", [(1024, 65536, 1023), (64, 4096, 63), (4096, 20000, 4095), (8, 704, 7),
                                         (1024, 20000, 5000), (256, 8200, 255)])
 def test_fir_block_f16_plan_equals_per_call(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, ns, waves):
@@ -358,7 +356,6 @@ def test_fir_block_f16_plan_equals_per_call(gpu_ctx, oracle, built_lib, kswitch,
     fp32 reference by the tolerance tests above."""
     kswitch("SDR_F16_MFMA", 1)
     kswitch("SDR_F16_W8", 1 if waves == "8" else 0)
-    kswitch("SDR_F16_R64", 1 if waves == "r64" else 0)
     sdrhip = built_lib
     rng = np.random.default_rng(ntaps + 7 * n)
     h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
@@ -381,20 +378,19 @@ def test_fir_block_f16_plan_equals_per_call(gpu_ctx, oracle, built_lib, kswitch,
         plan.close()
 
 
-@pytest.mark.parametrize("waves", ["8", "4", "r64"])
+@pytest.mark.parametrize("waves", ["8", "4"])
 @pytest.mark.parametrize("head", ["1", "0"])
 @pytest.mark.parametrize("ns", [1500, 5000])
 def test_fir_block_f16_long_state(gpu_ctx, oracle, built_lib, kswitch, ns, head, waves):
     """The MFMA fp16 arm with a carried state longer than T-1 (the first
     workgroup stages positions [-T, 0) of it and rewrites all ns, past its
     register slots through its loop), under both state-staging orders
-    (SDR_F16_HEAD) and every workgroup shape (SDR_F16_W8: 8 waves of one tile,
-    4 of two; SDR_F16_R64: 4 waves of 64-row tiles), two blocks: within the
-    tolerance of the exact fp32 filter, the state exact."""
+    (SDR_F16_HEAD) and both workgroup shapes (SDR_F16_W8: 8 waves of one tile,
+    4 of two), two blocks: within the tolerance of the exact fp32 filter, the
+    state exact."""
     kswitch("SDR_F16_MFMA", "1")
     kswitch("SDR_F16_HEAD", head)
     kswitch("SDR_F16_W8", "1" if waves == "8" else "0")
-    kswitch("SDR_F16_R64", "1" if waves == "r64" else "0")
     sdrhip = built_lib
     rng = np.random.default_rng(ns)
     ntaps, n, nstreams = 1024, 20000, 2
