@@ -369,7 +369,8 @@ struct MfArgs {
   int wg_per_stream;
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
   int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
-                          // 3 = no tap staging, 4 = no output stores, 7 = the head as interior, 8 = no head loads
+                          // 3 = no tap staging, 4 = no output stores, 7 = the head as interior, 8 = no head loads,
+                          // 10 = no head state stores, 11 = no head state LDS writes, 12 = 8 + 10, 13 = 8 + 10 + 11
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
   const _Float16* hplan;  // PLAN: the 8 tap copies (8 * lc halves) prebuilt by sdr_fir_f16_plan_create
   int ost;                // SDR_F16_TSTORE: LDS half offset of the per-wave output transpose areas
@@ -381,9 +382,17 @@ struct MfArgs {
 // barrier, 2 after the MFMA loop, 3 stores issued, 4 stores complete.
 #ifdef SDR_TIMING_BUILD
 constexpr int kMfTraceW = 40;
-#define MF_STAMP(k)                                                                          \
-  do {                                                                                       \
-    if (a.trace && lane == 0) a.trace[(long long)blockIdx.x * kMfTraceW + 8 * (k) + wave] = wall_clock64(); \
+// stamps held in registers and stored together at the end (a store per
+// stamp would be a vector-memory operation every later s_waitcnt vmcnt(0)
+// of the kernel waits for)
+#define MF_STAMP(k)                         \
+  do {                                      \
+    if (a.trace) mf_stamp[k] = wall_clock64(); \
+  } while (0)
+#define MF_STAMP_FLUSH()                                                                        \
+  do {                                                                                          \
+    if (a.trace && lane == 0)                                                                   \
+      for (int k_ = 0; k_ < 5; ++k_) a.trace[(long long)blockIdx.x * kMfTraceW + 8 * k_ + wave] = mf_stamp[k_]; \
   } while (0)
 #else
 #define MF_STAMP(k) \
@@ -415,10 +424,17 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int s = blockIdx.x / a.wg_per_stream;
-  const long long m0 = (long long)(blockIdx.x - s * a.wg_per_stream) * kMfOut;
+  // (timing ablation 14: each stream's workgroups in reverse order -- is a
+  // slow head workgroup its position in the grid or its work?)
+  const int wb = SDR_ABL(a.ablate) == 14 ? a.wg_per_stream - 1 - (int)(blockIdx.x - s * a.wg_per_stream)
+                                         : (int)(blockIdx.x - s * a.wg_per_stream);
+  const long long m0 = (long long)wb * kMfOut;
   const long long pb = m0 - a.ntaps;                   // stream position of image element 0 (multiple of 8)
   const _Float16* xs = a.x + (long long)s * a.x_stride;
   const _Float16* st = a.state + (long long)s * a.ns;
+#ifdef SDR_TIMING_BUILD
+  unsigned long long mf_stamp[5] = {0, 0, 0, 0, 0};
+#endif
   MF_STAMP(0);
   // ---- issue every load first (image chunks, taps), then write LDS: a
   // load-then-store loop waits out one memory latency per iteration.
@@ -426,25 +442,6 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // and kMfTaps the reversed taps (a.lc + 40 <= 4,424 halves).
   constexpr int kNT = 64 * kMfWaves, kMfChunks = (kMfOut + kMfMaxKd - 32 + 8 * kNT - 1) / (8 * kNT),
                 kMfTaps = (4424 + kNT - 1) / kNT;
-  // the stream's first workgroup (pb = -T, T <= 4096 = kMfSt * kNT): the
-  // carried state for image positions q in [-T, 0) and the new state (the
-  // block's last ns inputs, src/filter.cpp:82) join the same load batch, so
-  // this workgroup waits out one memory latency like the others, not three.
-  // Issued FIRST: they touch two pages no other workgroup does (the state
-  // buffer, the row's tail); issued after the image loads they left these
-  // workgroups staging 2.2 vs 1.0 us (phase trace, profiles/r05o/, r05p/)
-  constexpr int kMfSt = 4096 / kNT;
-  const bool head = a.head_pre && pb < 0 && SDR_ABL(a.ablate) != 7;  // (timing 7: head as interior)
-  _Float16 sv[kMfSt], nv[kMfSt];
-  if (head) {
-#pragma unroll
-    for (int k = 0; k < kMfSt; ++k) {
-      const int q = (int)pb + tid + k * kNT;
-      sv[k] = (q < 0 && q >= -a.ns && SDR_ABL(a.ablate) != 8) ? st[a.ns + q] : (_Float16)0;  // (8: no head loads)
-      const int i = tid + k * kNT;
-      nv[k] = (i < a.ns && SDR_ABL(a.ablate) != 8) ? xs[a.n - a.ns + i] : (_Float16)0;
-    }
-  }
   const int nchunk = a.span >> 3;
   // every register defined (clamped, in-bounds addresses: n >= 8 on this
   // path), so the array stays in VGPRs; the edge chunks are rewritten below
@@ -456,6 +453,24 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
     p = p < 0 ? 0 : (p > a.n - 8 ? a.n - 8 : p);
     if (SDR_ABL(a.ablate) == 1) p = 0;  // (ablation 1: one cached chunk instead of the stream)
     iv[k] = *reinterpret_cast<const u32x4*>(xs + (p & ~7LL));
+  }
+  // the stream's first workgroup (pb = -T, T <= 4096 = kMfSt * kNT): the
+  // carried state for image positions q in [-T, 0) and the new state (the
+  // block's last ns inputs, src/filter.cpp:82) join the same load batch, so
+  // this workgroup waits out one memory latency like the others, not three.
+  // The halves are held zero-extended in 32-bit registers: packed two to a
+  // register, each load would be waited for where it is packed
+  constexpr int kMfSt = 4096 / kNT;
+  const bool head = a.head_pre && pb < 0 && SDR_ABL(a.ablate) != 7;  // (timing 7: head as interior)
+  unsigned short sv[kMfSt], nv[kMfSt];  // raw fp16 bits
+  if (head) {
+#pragma unroll
+    for (int k = 0; k < kMfSt; ++k) {
+      const int q = (int)pb + tid + k * kNT;
+      sv[k] = (q < 0 && q >= -a.ns && SDR_ABL(a.ablate) != 8 && SDR_ABL(a.ablate) < 12) ? reinterpret_cast<const unsigned short*>(st)[a.ns + q] : (unsigned short)0;  // (8: no head loads)
+      const int i = tid + k * kNT;
+      nv[k] = (i < a.ns && SDR_ABL(a.ablate) != 8 && SDR_ABL(a.ablate) < 12) ? reinterpret_cast<const unsigned short*>(xs)[a.n - a.ns + i] : (unsigned short)0;
+    }
   }
   // the reversed f16 taps once, hb[j] = hr[j - 32], hr[v] = h[T-1-v]
   // (coalesced f32 loads); the tap copies are built from them in LDS below
@@ -484,7 +499,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
       const int q = (int)pb + tid + k * kNT;
-      if (q < 0 && SDR_ABL(a.ablate) != 11) img[mf_pad(q - (int)pb)] = sv[k];
+      if (q < 0 && SDR_ABL(a.ablate) != 11 && SDR_ABL(a.ablate) != 13) reinterpret_cast<unsigned short*>(img)[mf_pad(q - (int)pb)] = sv[k];
     }
   }
   // block edges (the stream's first and last workgroups), element-wise over
@@ -512,10 +527,10 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // the stream's first workgroup is the only reader of the old state (staged
   // above): it writes the new one, the block's last ns inputs
   // (src/filter.cpp:82), after that barrier
-  if (head && SDR_ABL(a.ablate) != 10) {  // (timing 10: no new-state stores; 11: no state LDS writes)
+  if (head && SDR_ABL(a.ablate) != 10 && SDR_ABL(a.ablate) < 12) {  // (timing 10 / 12+: no new-state stores)
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k)
-      if (tid + k * kNT < a.ns) a.state[(long long)s * a.ns + tid + k * kNT] = nv[k];
+      if (tid + k * kNT < a.ns) reinterpret_cast<unsigned short*>(a.state)[(long long)s * a.ns + tid + k * kNT] = nv[k];
     for (int i = tid + kMfSt * kNT; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
   } else if (m0 == 0 && SDR_ABL(a.ablate) != 7) {
     for (int i = tid; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
@@ -636,6 +651,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   MF_STAMP(3);
   if (a.trace) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   MF_STAMP(4);
+  MF_STAMP_FLUSH();
 #endif
 }
 

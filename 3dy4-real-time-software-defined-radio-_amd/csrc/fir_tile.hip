@@ -79,6 +79,12 @@
 #endif
 // (Round 5: the wire-byte unpack with packed FMAs, v_pk_fma_f32 for two
 // samples, measured neutral on cfg2u8 and -1.5 % on mono0; code at 821f6db.)
+// SDR_SC_T0PRE: fir_tile_sc's tile 0 issues its extra loads (carried state,
+// block tail, side copy) with the span's (one memory latency, not three);
+// f32 front end: cfg2 0.0954-0.0959 vs 0.0959-0.0963 ms (profiles/r05u/)
+#ifndef SDR_SC_T0PRE
+#define SDR_SC_T0PRE 1
+#endif
 // SDR_SCAN_VCONST (timing builds only, wrong outputs): fir_tile_sc's scan
 // with a VGPR in place of the SGPR taps
 #ifndef SDR_SCAN_VCONST
@@ -164,13 +170,12 @@ __device__ __forceinline__ float demod_one(float I, float Q, float ip, float qp)
 // stores after their s_waitcnt(0) -- one memory latency for both, not two.
 constexpr int kSideMax = 4;
 __device__ __forceinline__ void side_load(const FirLaunch& a, int s, int tid, int nth, float (&v)[kSideMax]) {
+  if (a.side_n <= 0) return;  // launch-uniform
   const float* src = a.side_src + (long long)s * a.side_src_stride;
+  // unguarded loads at clamped indices (side_store skips the extra lanes): an
+  // exec-masked load's merge would make the compiler wait for it right here
 #pragma unroll
-  for (int u = 0; u < kSideMax; ++u) {
-    const int j = tid + u * nth;
-    v[u] = 0.0f;
-    if (j < a.side_n) v[u] = src[j];
-  }
+  for (int u = 0; u < kSideMax; ++u) v[u] = src[min(tid + u * nth, a.side_n - 1)];
 }
 __device__ __forceinline__ void side_store(const FirLaunch& a, int s, int tid, int nth, const float (&v)[kSideMax]) {
   float* dst = a.side_dst + (long long)s * a.side_dst_stride;
@@ -1306,14 +1311,49 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     const int s = __builtin_amdgcn_readfirstlane(tr.s);
     old_pi = ((cf)a.prev0)[s];
     old_pq = ((cf)a.prev1)[s];
+#if !SDR_SC_T0PRE
     // both read before the barrier below: wave 1 rewrites prev_Q after it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
   }
   using Stage = float4[G::FULL + 1];
   Stage v;
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (SDR_ABL(a.ablate) != 1) stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
+  // Tile 0's own inputs go out in the span's load batch (SDR_SC_T0PRE): the
+  // carried state under the span's head, the block's last STRIP inputs (the
+  // prev_* recompute and the new state) and the side copy -- one memory
+  // latency for the tile instead of three (edge loads after the span landed,
+  // strip loads after the scan).  Needs the span's top inside the block
+  // (t0pre); else tile 0 takes edge_fill and the strip loads as before.
+  constexpr int kPre = (G::STRIP > G::HALO ? G::STRIP : G::HALO) / 64 + 1;
+  constexpr int kTp = (T + 63) / 64;  // taps per lane for the prev_* recompute's products
+  float e_pre[kPre], s_pre[kPre], side[kSideMax], h_pre[kTp];
+  // (f32 only: on the u8 wire path it measured 0.5-1 % slower -- its byte
+  // loads of the tail; profiles/r05u/ab_t0pre.txt)
+  const bool t0pre = SDR_SC_T0PRE && SRC == Src::F32 && t0x && ns <= G::STRIP && ns >= (int)-tr.pb &&
+                     n >= G::STRIP &&
+                     ((n & 3) == 0 || tr.pb + G::LDS_LEN <= (n & ~3LL));  // workgroup-uniform
+  if (t0pre) {
+#pragma unroll
+    // unguarded loads at clamped indices (the extra lanes' values are never
+    // used): no exec-masked load whose merge would make the compiler wait
+    for (int u = 0; u < kPre; ++u) {
+      const int i = lane + 64 * u;
+      e_pre[u] = tr.st0[ns + tr.pb + min(i, (int)-tr.pb - 1)];  // pb = -HALO >= -ns (t0pre)
+      // the block's tail (n >= STRIP: inside the block): raw loads, converted
+      // where they are stored (a u8 conversion here would wait on each load)
+      const long long pt = n - G::STRIP + min(i, G::STRIP - 1);
+      if constexpr (SRC == Src::F32)
+        s_pre[u] = tr.x0[pt];
+      else
+        s_pre[u] = __uint_as_float((uint32_t)tr.iq[2 * pt + c]);
+    }
+    if (c == 0) side_load(a, tr.s, lane, 64, side);
+#pragma unroll
+    for (int u = 0; u < kTp; ++u) h_pre[u] = h[min(lane + 64 * u, T - 1)];
+  }
   if constexpr (SRC == Src::F32) {
     stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds, lds, lane, v, v);
   } else {
@@ -1332,7 +1372,13 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     for (int it = 0; it < G::FULL; ++it) put(lane + it * NTH, v[it]);
     if (G::REM && lane < G::REM) put(lane + G::FULL * NTH, v[G::FULL]);
   }
-  if (t0x || (tr.t != 0 && !interior<D, T, R, DEMOD, NW>(tr, n))) {
+  if (t0pre) {
+    // the span's head: the carried state (the clamped chunks there loaded
+    // block data), written after this wave's chunk stores to the same slice
+#pragma unroll
+    for (int u = 0; u < kPre; ++u)
+      if (lane + 64 * u < (int)-tr.pb) lds[lane + 64 * u] = e_pre[u];
+  } else if (t0x || (tr.t != 0 && !interior<D, T, R, DEMOD, NW>(tr, n))) {
     wave_sync();
     edge_fill<D, T, R, DEMOD, NW, 1, SRC>(tr, lane, n, ns, [&](int i, float v0, float) { lds[i] = v0; }, c);
   }
@@ -1349,6 +1395,10 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
 #pragma unroll
     for (int r = 0; r < R; ++r) xch[r * 64 + lane] = acc[r];
   }
+#if SDR_SC_T0PRE
+  // prev_I / prev_Q read before the barrier: wave 1 rewrites prev_Q after it
+  if (c == 0 && t0x) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
   __syncthreads();
   if (c == 0) {
     float accQ[R];
@@ -1392,35 +1442,58 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   }
   // state carry (tile 0): each wave its own channel, after every read of the old values
   if (t0x) {
-    float side[kSideMax];
-    if (c == 0) side_load(a, tr.s, lane, 64, side);
     float* strip = lds;  // the scan is done with it
-    for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
-      float w[4];
+    if (t0pre) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u * NTH + lane;
-        w[u] = j < G::STRIP ? edge_at<SRC>(tr.x0, tr.iq, c, tr.st0, ns, n, n - G::STRIP + j) : 0.0f;
-      }
+      for (int u = 0; u < kPre; ++u)
+        if (lane + 64 * u < G::STRIP)
+          strip[lane + 64 * u] = SRC == Src::F32 ? s_pre[u] : u8_to_f32(__float_as_uint(s_pre[u]));
+    } else {
+      if (c == 0) side_load(a, tr.s, lane, 64, side);
+      for (int j0 = 0; j0 < G::STRIP; j0 += 4 * NTH) {
+        float w[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u * NTH + lane;
-        if (j < G::STRIP) strip[j] = w[u];
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * NTH + lane;
+          w[u] = j < G::STRIP ? edge_at<SRC>(tr.x0, tr.iq, c, tr.st0, ns, n, n - G::STRIP + j) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * NTH + lane;
+          if (j < G::STRIP) strip[j] = w[u];
+        }
       }
+      __builtin_amdgcn_s_waitcnt(0);
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    // (t0pre: no load is outstanding here -- no drain, which would also wait
+    // out the tile's output stores just issued)
     if (c == 0) side_store(a, tr.s, lane, 64, side);
     wave_sync();
-    if (lane == 0) {
+    {
       // prev_c <- this channel's last decimated output (src/filter.cpp:100-101),
-      // recomputed in the reference's order from the strip
-      using hconst = const __attribute__((address_space(4))) float*;
-      const hconst hc = (hconst)h;
+      // recomputed in the reference's order from the strip: the T products
+      // h[k] * x[n-D-k] by all lanes at once (each rounded as the reference
+      // rounds it), then lane 0 sums them for k = 0..T-1 -- the chain is the
+      // adds alone
+      static_assert(T <= G::LDS_LEN - G::STRIP, "the products fit the slice after the strip");
+      float* prod = strip + G::STRIP;
       const float* sp = strip + (G::STRIP - D);
-      float y = 0.0f;
+      if (!t0pre) {
+#pragma unroll
+        for (int u = 0; u < kTp; ++u) h_pre[u] = lane + 64 * u < T ? h[lane + 64 * u] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kTp; ++u) {
+        const int k = lane + 64 * u;
+        if (k < T) prod[k] = h_pre[u] * sp[-k];
+      }
+      wave_sync();
+      if (lane == 0) {
+        float y = 0.0f;
 #pragma unroll 8
-      for (int k = 0; k < T; ++k) y = y + hc[k] * sp[-k];
-      (c ? a.prev1 : a.prev0)[tr.s] = y;
+        for (int k = 0; k < T; ++k) y = y + prod[k];
+        (c ? a.prev1 : a.prev0)[tr.s] = y;
+      }
     }
     if (ns <= G::STRIP) {
       for (int j = lane; j < ns; j += NTH) tr.st0[j] = strip[G::STRIP - ns + j];
