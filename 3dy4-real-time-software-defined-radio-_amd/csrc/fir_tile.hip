@@ -813,6 +813,11 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SDR_FIR_LB
 #define SDR_FIR_LB 1024
 #endif
+// SDR_GRP_T0PRE: fir_tile_grp's one-channel f32 tile 0 loads its extra inputs
+// (carried state, new state, side copy) before the span's wait
+#ifndef SDR_GRP_T0PRE
+#define SDR_GRP_T0PRE 1
+#endif
 // fir_tile_grp's LDS floats per wave: one span per channel (a one-channel
 // FIR needs half of fir_tile's two-channel slice: 16 waves of the D = 5 / 1
 // FIRs fit a CU instead of 14, one round of tiles instead of two)
@@ -962,13 +967,34 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
     // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) before it
     // rewrites the state below.
     SDR_TRACE_AT(0);
+    // A one-channel f32 FIR's tile 0 (SDR_GRP_T0PRE): the carried state under
+    // the span's head, the new state (the block's last ns inputs) and the side
+    // copy as unguarded loads at clamped indices here, before the span's wait
+    // -- instead of an edge pass after it and the tail loads after the scan
+    constexpr int kPre = (G::HALO > 64 * kSideMax ? G::HALO : 64 * kSideMax) / 64 + 1;
+    float e_pre[kPre], n_pre[kPre], side[kSideMax];
+    const bool t0pre = SDR_GRP_T0PRE && !DEMOD && NCH == 1 && SRC == Src::F32 && tr.t == 0 && ns >= (int)-tr.pb &&
+                       ns <= 64 * kPre && n >= ns && ((n & 3) == 0 || tr.pb + G::LDS_LEN <= (n & ~3LL));
+    if (t0pre) {
+#pragma unroll
+      for (int u = 0; u < kPre; ++u) {
+        const int i = tid + 64 * u;
+        e_pre[u] = tr.st0[ns + tr.pb + min(i, (int)-tr.pb - 1)];
+        n_pre[u] = tr.x0[n - ns + min(i, ns - 1)];
+      }
+      side_load(a, tr.s, tid, NTH, side);
+    }
     wave_sync();
 #ifdef SDR_FIR_TRACE
     __builtin_amdgcn_s_waitcnt(0);
     SDR_TRACE_AT(1);
 #endif
     stage_store<D, T, R, DEMOD, NW, NCH, SRC>(lds0, lds1, tid, v0, v1);
-    if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
+    if (t0pre) {
+#pragma unroll
+      for (int u = 0; u < kPre; ++u)
+        if (tid + 64 * u < (int)-tr.pb) lds0[tid + 64 * u] = e_pre[u];
+    } else if (tr.t == 0 || !interior<D, T, R, DEMOD, NW>(tr, n)) {  // workgroup-uniform
       wave_sync();
       edge_fill<D, T, R, DEMOD, NW, NCH, SRC>(tr, tid, n, ns, [&](int i, float v0, float v1) {
         lds0[i] = v0;
@@ -1103,8 +1129,13 @@ __global__ __launch_bounds__(SDR_FIR_LB) void fir_tile_grp(FirLaunch a, const fl
 
     // ---- 4. state carry (tile 0 only; every read of the old values
     // happened before the barriers above)
-    if (tr.t == 0) {
-      float side[kSideMax];
+    if (t0pre) {
+      // the new state and the side copy straight from registers (no strip)
+      side_store(a, tr.s, tid, NTH, side);
+#pragma unroll
+      for (int u = 0; u < kPre; ++u)
+        if (tid + 64 * u < ns) tr.st0[tid + 64 * u] = n_pre[u];
+    } else if (tr.t == 0) {
       side_load(a, tr.s, tid, NTH, side);
       // stage the block's last STRIP inputs (old state where p < 0: the
       // D*(nout-1) - k >= -(T-1) >= -ns inputs of the last output) into the

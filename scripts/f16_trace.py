@@ -60,6 +60,11 @@ for r, t in enumerate(rows):
     worst = np.argsort(stw)[-6:][::-1]
     print("  slowest staging (workgroup: us):", ", ".join(f"{w}: {stw[w]:.2f}" for w in worst),
           "| workgroup 0:", f"{stw[0]:.2f}", "| last of stream 0:", f"{stw[t.shape[0] // 2 - 1]:.2f}")
+    for w in (0, 1, t.shape[0] // 2):
+        e = (t[w, 0, :] - t[w, 0, :].min()) * 10e-3
+        b = (t[w, 1, :] - t[w, 0, :].min()) * 10e-3
+        print(f"  workgroup {w}: wave entries +" + " ".join(f"{v:.2f}" for v in e) + " | past barrier +" +
+              " ".join(f"{v:.2f}" for v in b))
     wg_first = t[:, 0, :].min(axis=1)
     order = np.argsort(wg_first)
     print("  last-entry workgroups:", order[-4:].tolist(), "first-entry:", order[:4].tolist())
