@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   constexpr int kMfSt = 4096 / kNT;
   const bool head = a.head_pre && pb < 0 && SDR_ABL(a.ablate) != 7;  // (timing 7: head as interior)
   unsigned short sv[kMfSt], nv[kMfSt];  // raw fp16 bits
-  if (head) {
+  if (head && SDR_ABL(a.ablate) != 16) {  // (timing 16: the head's load block not even issued)
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
       const int q = (int)pb + tid + k * kNT;
@@ -493,13 +493,14 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
 #pragma unroll
   for (int k = 0; k < kMfChunks; ++k) {
     const int c = tid + k * kNT;
-    if (c < nchunk && !(head && pb + 8LL * c < 0)) *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
+    if (c < nchunk && !(head && pb + 8LL * c < 0 && SDR_ABL(a.ablate) != 15))  // (15: every chunk written)
+      *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
   }
   if (head) {
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
       const int q = (int)pb + tid + k * kNT;
-      if (q < 0 && SDR_ABL(a.ablate) != 11 && SDR_ABL(a.ablate) != 13) reinterpret_cast<unsigned short*>(img)[mf_pad(q - (int)pb)] = sv[k];
+      if (q < 0 && SDR_ABL(a.ablate) != 11 && SDR_ABL(a.ablate) < 13) reinterpret_cast<unsigned short*>(img)[mf_pad(q - (int)pb)] = sv[k];
     }
   }
   // block edges (the stream's first and last workgroups), element-wise over
