@@ -369,8 +369,7 @@ struct MfArgs {
   int wg_per_stream;
   int span;               // staged input halves per workgroup (kMfOut + kd - 32)
   int ablate;             // timing ablations only (SDR_ABLATE): 1 = one cached input chunk, 2 = no MFMA,
-                          // 3 = no tap staging, 4 = no output stores, 7 = the head as interior, 8 = no head loads,
-                          // 10 = no head state stores, 11 = no head state LDS writes, 12 = 8 + 10, 13 = 8 + 10 + 11
+                          // 3 = no tap staging, 4 = no output stores, 7 = the head as interior, 14 = reversed grid
   int head_pre;           // the first workgroup's state loads in the first load batch (SDR_F16_HEAD, A/B)
   const _Float16* hplan;  // PLAN: the 8 tap copies (8 * lc halves) prebuilt by sdr_fir_f16_plan_create
   int ost;                // SDR_F16_TSTORE: LDS half offset of the per-wave output transpose areas
@@ -458,18 +457,29 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // carried state for image positions q in [-T, 0) and the new state (the
   // block's last ns inputs, src/filter.cpp:82) join the same load batch, so
   // this workgroup waits out one memory latency like the others, not three.
-  // The halves are held zero-extended in 32-bit registers: packed two to a
-  // register, each load would be waited for where it is packed
+  // The halves are held zero-extended in 32-bit registers (packed two to a
+  // register, each load would be waited for where it is packed), and each
+  // loop runs only the rows k that hold some lane's element -- a uniform
+  // bound: a load issued with EXEC = 0 still costs the CU's address path,
+  // and 12 of the 16 loads per thread at T = 1024 were such (0.8 us of this
+  // workgroup's 2.3 us of staging, phase trace profiles/r05z/)
   constexpr int kMfSt = 4096 / kNT;
   const bool head = a.head_pre && pb < 0 && SDR_ABL(a.ablate) != 7;  // (timing 7: head as interior)
+  const int kst = (int)((-pb + kNT - 1) / kNT);                      // rows of positions [-T, 0)
+  const int knv = (a.ns + kNT - 1) / kNT < kMfSt ? (a.ns + kNT - 1) / kNT : kMfSt;  // rows of the new state
   unsigned short sv[kMfSt], nv[kMfSt];  // raw fp16 bits
-  if (head && SDR_ABL(a.ablate) != 16) {  // (timing 16: the head's load block not even issued)
+  if (head) {
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
+      if (k >= kst) break;
       const int q = (int)pb + tid + k * kNT;
-      sv[k] = (q < 0 && q >= -a.ns && SDR_ABL(a.ablate) != 8 && SDR_ABL(a.ablate) < 12) ? reinterpret_cast<const unsigned short*>(st)[a.ns + q] : (unsigned short)0;  // (8: no head loads)
+      sv[k] = (q < 0 && q >= -a.ns) ? reinterpret_cast<const unsigned short*>(st)[a.ns + q] : (unsigned short)0;
+    }
+#pragma unroll
+    for (int k = 0; k < kMfSt; ++k) {
+      if (k >= knv) break;
       const int i = tid + k * kNT;
-      nv[k] = (i < a.ns && SDR_ABL(a.ablate) != 8 && SDR_ABL(a.ablate) < 12) ? reinterpret_cast<const unsigned short*>(xs)[a.n - a.ns + i] : (unsigned short)0;
+      nv[k] = i < a.ns ? reinterpret_cast<const unsigned short*>(xs)[a.n - a.ns + i] : (unsigned short)0;
     }
   }
   // the reversed f16 taps once, hb[j] = hr[j - 32], hr[v] = h[T-1-v]
@@ -493,14 +503,14 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
 #pragma unroll
   for (int k = 0; k < kMfChunks; ++k) {
     const int c = tid + k * kNT;
-    if (c < nchunk && !(head && pb + 8LL * c < 0 && SDR_ABL(a.ablate) != 15))  // (15: every chunk written)
-      *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
+    if (c < nchunk && !(head && pb + 8LL * c < 0)) *reinterpret_cast<u32x4*>(img + mf_pad(8 * c)) = iv[k];
   }
   if (head) {
 #pragma unroll
     for (int k = 0; k < kMfSt; ++k) {
+      if (k >= kst) break;
       const int q = (int)pb + tid + k * kNT;
-      if (q < 0 && SDR_ABL(a.ablate) != 11 && SDR_ABL(a.ablate) < 13) reinterpret_cast<unsigned short*>(img)[mf_pad(q - (int)pb)] = sv[k];
+      if (q < 0) reinterpret_cast<unsigned short*>(img)[mf_pad(q - (int)pb)] = sv[k];
     }
   }
   // block edges (the stream's first and last workgroups), element-wise over
@@ -528,10 +538,12 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   // the stream's first workgroup is the only reader of the old state (staged
   // above): it writes the new one, the block's last ns inputs
   // (src/filter.cpp:82), after that barrier
-  if (head && SDR_ABL(a.ablate) != 10 && SDR_ABL(a.ablate) < 12) {  // (timing 10 / 12+: no new-state stores)
+  if (head) {
 #pragma unroll
-    for (int k = 0; k < kMfSt; ++k)
+    for (int k = 0; k < kMfSt; ++k) {
+      if (k >= knv) break;
       if (tid + k * kNT < a.ns) reinterpret_cast<unsigned short*>(a.state)[(long long)s * a.ns + tid + k * kNT] = nv[k];
+    }
     for (int i = tid + kMfSt * kNT; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
   } else if (m0 == 0 && SDR_ABL(a.ablate) != 7) {
     for (int i = tid; i < a.ns; i += kNT) a.state[(long long)s * a.ns + i] = xs[a.n - a.ns + i];
