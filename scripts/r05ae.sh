@@ -1,0 +1,14 @@
+#!/bin/bash
+# r05ae: fir_long_mfma with two accumulator chains per tile (even / odd
+# k-steps): f16 parity, same-box A/B vs one chain (ab/acc1.so =
+# SDR_F16_ACC2=0), timed rocprof of cfg5h.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r05ae; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q \
+  -p no:cacheprovider --timeout 200 --timeout-method thread -k "f16 or cfg5h" > $OUT/pytest.log 2>&1; rc=$?
+tail -1 $OUT/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest.log | head -20; exit $rc; }
+ARMS="tree ab/acc1.so" CFGS="cfg5h" REPS=4 bash scripts/ab_libs.sh > $OUT/ab.txt 2>&1; rc=$?; cat $OUT/ab.txt; [ $rc -eq 0 ] || exit $rc
+TAG=r05ae CFGS="cfg5h" bash scripts/prof_cfg.sh || exit 1
+find $OUT -name '*kernel_trace.csv' -delete
+exit 0
