@@ -214,3 +214,24 @@ def test_cpu_baseline_every_config(config):
         assert res["pcm_ok"]
     if config == "cfg2":
         assert "cfg1" in res or res["kind"] == "port"
+
+
+@pytest.mark.parametrize("config", ["cfg2", "cfg2u8", "cfg3", "cfg4", "cfg4x8", "cfg5", "cfg5h", "mono0"])
+def test_traffic_record_for_every_hbm_config(config):
+    """Every config whose line prices HBM carries a PMC traffic record
+    (profiles/traffic_<cfg>.json, FETCH_SIZE x2 + WRITE_SIZE per launch), and
+    roofline() attaches it; against the closing record's algorithmic bytes it
+    sits between 1x (every input fetched once) and the documented re-reads
+    (cfg5's staged halo 1.52x, cfg5h's 1.19x, mono0's demod row 1.45x,
+    DESIGN.md 5.1)."""
+    import json
+
+    b = _bench()
+    with open(os.path.join(REPO, "profiles", f"traffic_{config}.json")) as f:
+        t = json.load(f)["hbm_bytes_per_launch"]
+    assert isinstance(t, int) and t > 0
+    with open(os.path.join(REPO, "profiles", "r05ad", f"bench_{config}.json")) as f:
+        alg = json.load(f)["roofline"]["algorithmic_bytes_per_launch"]
+    assert 0.98 <= t / alg <= {"cfg5": 1.6, "mono0": 1.6, "cfg5h": 1.25}.get(config, 1.1)
+    job = {"units": alg, "bytes_per_pair": 1.0, "flops_per_unit": 1.0, "kind": "frontend_f32"}
+    assert b.roofline(job, 0.1, config)["traffic"] == t
