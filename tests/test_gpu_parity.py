@@ -9,6 +9,8 @@ the discriminator), so no tolerance is needed.  For sizes where the oracle
 would be too slow, size-independent properties are checked instead
 (stream/shard permutation invariance, block-size independence).
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -931,3 +933,90 @@ def test_fir_long_8192_taps_both_tap_modes(gpu_ctx, oracle, built_lib, kswitch):
             for s in range(S):
                 assert_bits(got[s], oracle.fir_block(x[s], h, ost[s]), f"vtap {vtap} stream {s} block {b}")
             assert_bits(d_st.download().reshape(S, ns), np.stack(ost), f"vtap {vtap} state block {b}")
+
+
+# ------------------------------------------------ seeded random shape sweep
+# Shapes drawn once from a fixed seed (the same list every run): decimation
+# 1-12, tap counts 1-320 odd and even, state lengths from T-1 to T+63, block
+# lengths from one output to ~20 k samples, three consecutive blocks each so
+# the carried state is exercised -- every kernel choice the dispatcher makes
+# (tiled, split-channel, generic, long) meets shapes no hand-written case
+# picked.  Bitwise against the oracle, outputs and state.  Shapes the
+# reference cannot run (block shorter than the state, n*up/down fractional)
+# are refused by the library and are kept out of the draw.
+_RNG = np.random.default_rng(20261018)
+_DECIM = []
+for _ in range(24):
+    _D = int(_RNG.integers(1, 13))
+    _T = int(_RNG.choice([int(_RNG.integers(1, 40)), int(_RNG.integers(40, 321)), 101, 64, 128]))
+    _ns = _T - 1 + int(_RNG.integers(0, 64))
+    _n = _D * int(_RNG.choice([1, int(_RNG.integers(2, 300)), int(_RNG.integers(300, 2000))]))
+    _ns = max(_ns, 0)
+    _n = max(_n, (_ns + _D - 1) // _D * _D)  # block >= state (filter.cpp:139's precondition, refused otherwise)
+    _DECIM.append((_D, _T, _ns, _n))
+_RES = []
+for _ in range(12):
+    _up, _down = int(_RNG.integers(1, 12)), int(_RNG.integers(1, 40))
+    _T = _up * int(_RNG.integers(2, 120)) + int(_RNG.integers(0, _up))
+    _ns = (_T + _up - 1) // _up - 1 + int(_RNG.integers(0, 8))
+    _q = _down // math.gcd(_up, _down)  # n*up/down whole (filter.cpp:149-162's loop bound, refused otherwise)
+    _n = _q * max(1, int(_RNG.integers(1, 6000)) // _q)
+    _n = max(_n, (_ns + _q - 1) // _q * _q)
+    _RES.append((_up, _down, _T, max(_ns, 1), _n))
+
+_FRONT = []
+for _ in range(12):
+    _D = int(_RNG.choice([1, 2, 4, 5, 8, 10, 10, 12]))
+    _T = int(_RNG.choice([101, 101, int(_RNG.integers(2, 200))]))
+    _ns = _T - 1 + int(_RNG.integers(0, 40))
+    _n = _D * max(int(_RNG.integers(1, 3000)), (_ns + _D - 1) // _D)
+    _FRONT.append((_D, _T, _ns, _n))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,ntaps,ns,n", _FRONT, ids=[f"D{d}-T{t}-ns{s}-n{n}" for d, t, s, n in _FRONT])
+def test_frontend_random_shapes(gpu_ctx, oracle, D, ntaps, ns, n):
+    """The fused front end (FIR + decimate on I and Q, then the
+    discriminator), f32 planar and u8 wire input, three blocks each."""
+    from sdrhip.synth import fm_iq_u8
+
+    rng = np.random.default_rng(D * 131 + ntaps * 7 + n)
+    h = (rng.standard_normal(ntaps) / ntaps).astype(np.float32)
+    iq = fm_iq_u8(n * 3, seed=int(rng.integers(1 << 30)))
+    st = {k: [np.zeros(ns, np.float32), np.zeros(ns, np.float32), np.zeros(2, np.float32)]
+          for k in ("f32", "u8", "oracle")}
+    for b in range(3):
+        blk = iq[2 * n * b:2 * n * (b + 1)]
+        I, Q = oracle.u8_to_planar(blk)
+        want = oracle.frontend(D, I, Q, h, *st["oracle"])
+        assert_bits(gpu_ctx.frontend(D, I, Q, h, *st["f32"]), want, f"f32 block {b}")
+        assert_bits(gpu_ctx.frontend_u8(D, blk, h, *st["u8"]), want, f"u8 block {b}")
+        for k in ("f32", "u8"):
+            for got, ref, what in zip(st[k], st["oracle"], ("state_i", "state_q", "prev")):
+                assert_bits(got, ref, f"{k} {what} block {b}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,ntaps,ns,n", _DECIM, ids=[f"D{d}-T{t}-ns{s}-n{n}" for d, t, s, n in _DECIM])
+def test_fir_decim_random_shapes(gpu_ctx, oracle, D, ntaps, ns, n):
+    rng = np.random.default_rng(D * 7919 + ntaps * 31 + n)
+    h = (rng.standard_normal(ntaps) / max(ntaps, 1)).astype(np.float32)
+    s_g = rng.standard_normal(ns).astype(np.float32)
+    s_o = s_g.copy()
+    for blk in range(3):
+        x = rng.standard_normal(n).astype(np.float32)
+        assert_bits(gpu_ctx.fir_decim(D, x, h, s_g), oracle.fir_decim(D, x, h, s_o), f"block {blk}")
+        assert_bits(s_g, s_o, f"state after block {blk}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("up,down,ntaps,ns,n", _RES, ids=[f"L{u}-M{d}-T{t}-ns{s}-n{n}" for u, d, t, s, n in _RES])
+def test_resample_random_shapes(gpu_ctx, oracle, up, down, ntaps, ns, n):
+    rng = np.random.default_rng(up * 104729 + down * 31 + ntaps)
+    h = (rng.standard_normal(ntaps) / 20).astype(np.float32)
+    s_g = rng.standard_normal(ns).astype(np.float32)
+    s_o = s_g.copy()
+    for blk in range(3):
+        x = rng.standard_normal(n).astype(np.float32)
+        assert_bits(gpu_ctx.resample(up, down, x, h, s_g), oracle.resample(up, down, x, h, s_o), f"block {blk}")
+        assert_bits(s_g, s_o, f"state after block {blk}")
