@@ -1020,3 +1020,63 @@ def test_resample_random_shapes(gpu_ctx, oracle, up, down, ntaps, ns, n):
         x = rng.standard_normal(n).astype(np.float32)
         assert_bits(gpu_ctx.resample(up, down, x, h, s_g), oracle.resample(up, down, x, h, s_o), f"block {blk}")
         assert_bits(s_g, s_o, f"state after block {blk}")
+
+
+_BATCH = []
+for _ in range(12):
+    _D = int(_RNG.choice([1, 2, 4, 5, 10, 10, 8]))
+    _T = int(_RNG.choice([101, int(_RNG.integers(2, 160))]))
+    _ns = _T - 1 + int(_RNG.integers(0, 20))
+    _n = _D * max(int(_RNG.integers(1, 2500)), (_ns + _D - 1) // _D)
+    _BATCH.append((_D, _T, _ns, _n, int(_RNG.integers(1, 8)), int(_RNG.integers(0, 8)), int(_RNG.integers(0, 6))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,ntaps,ns,n,nstreams,xpad,ypad", _BATCH,
+                         ids=[f"D{d}-T{t}-ns{s}-n{n}-S{k}-px{p}-py{q}" for d, t, s, n, k, p, q in _BATCH])
+def test_batched_random_shapes(gpu_ctx, oracle, built_lib, D, ntaps, ns, n, nstreams, xpad, ypad):
+    """The device-resident batched calls on random shapes: nstreams rows
+    with padded strides (aligned or not -- the dispatcher's fast or generic
+    path), FIR + decimate on f32 rows and the fused u8 front end, three
+    blocks, every stream and state bitwise against the oracle."""
+    sdrhip = built_lib
+    rng = np.random.default_rng(D * 17 + ntaps * 3 + n + nstreams)
+    h = (rng.standard_normal(ntaps) / ntaps).astype(np.float32)
+    nout = n // D
+    xs, ys = n + xpad, nout + ypad
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    # FIR + decimate, f32 rows
+    st = rng.standard_normal((nstreams, ns)).astype(np.float32)
+    ref_st = st.copy()
+    d_s = sdrhip.DeviceArray.from_numpy(gpu_ctx, st)
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * ys * 4)
+    for b in range(3):
+        x = rng.standard_normal((nstreams, xs)).astype(np.float32)
+        d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+        gpu_ctx.fir_decim_dev(D, d_x, n, nstreams, xs, d_h, ntaps, d_s, ns, d_y, ys)
+        gpu_ctx.synchronize()
+        y = d_y.download().reshape(nstreams, ys)[:, :nout]
+        for s in range(nstreams):
+            assert_bits(y[s], oracle.fir_decim(D, x[s, :n], h, ref_st[s]), f"fir stream {s} block {b}")
+        assert_bits(d_s.download().reshape(nstreams, ns), ref_st, f"fir state block {b}")
+    # fused u8 front end (IQ rows of 2n bytes + an even pad)
+    iqs = 2 * n + 2 * xpad
+    iq = _fm_streams(nstreams, (iqs // 2) * 3 + 1, seed=int(rng.integers(1 << 30)))
+    z = lambda *shape: sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(shape, np.float32))  # noqa: E731
+    d_si, d_sq, d_pi, d_pq = z(nstreams, ns), z(nstreams, ns), z(nstreams), z(nstreams)
+    ors = [dict(si=np.zeros(ns, np.float32), sq=np.zeros(ns, np.float32), prev=np.zeros(2, np.float32))
+           for _ in range(nstreams)]
+    for b in range(3):
+        blk = np.ascontiguousarray(iq[:, iqs * b:iqs * (b + 1)])
+        d_iq = sdrhip.DeviceArray.from_numpy(gpu_ctx, blk)
+        gpu_ctx.frontend_u8_dev(D, d_iq, n, nstreams, iqs, d_h, ntaps, d_si, d_sq, ns, d_pi, d_pq, d_y, ys)
+        gpu_ctx.synchronize()
+        got = d_y.download().reshape(nstreams, ys)[:, :nout]
+        for s in range(nstreams):
+            Is, Qs = oracle.u8_to_planar(blk[s, :2 * n])
+            want = oracle.frontend(D, Is, Qs, h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"])
+            assert_bits(got[s], want, f"u8 stream {s} block {b}")
+        assert_bits(d_si.download().reshape(nstreams, ns), np.stack([o["si"] for o in ors]), f"state_i block {b}")
+        assert_bits(d_sq.download().reshape(nstreams, ns), np.stack([o["sq"] for o in ors]), f"state_q block {b}")
+        assert_bits(d_pi.download(), np.array([o["prev"][0] for o in ors], np.float32), f"prev_i block {b}")
+        assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), f"prev_q block {b}")
