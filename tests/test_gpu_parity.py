@@ -283,10 +283,13 @@ def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, 
     exact sum over the fp16-rounded operands.  The carried fp16 state is the
     last ns inputs, exactly."""
     kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
-    sdrhip = built_lib
-    rng = np.random.default_rng(ntaps + n)
+    _f16_tolerance_check(gpu_ctx, oracle, built_lib, ntaps, n, 2, ntaps + n)
+
+
+def _f16_tolerance_check(gpu_ctx, oracle, sdrhip, ntaps, n, nstreams, seed):
+    rng = np.random.default_rng(seed)
     h = oracle.taps_lpf(2.4e6, 100e3, ntaps, 1)
-    ns, nstreams = ntaps - 1, 2
+    ns = ntaps - 1
     st_ref = [np.zeros(ns, np.float32) for _ in range(nstreams)]
     d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
     sth = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.zeros(nstreams * ns, np.float16))
@@ -295,8 +298,11 @@ def test_fir_block_f16_tolerance(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, 
     prev16 = [np.zeros(ns, np.float64) for _ in range(nstreams)]
     for blk in range(2):
         x = rng.standard_normal((nstreams, n)).astype(np.float32)
-        xh = sdrhip.DeviceArray.from_numpy(gpu_ctx, x.astype(np.float16))
-        gpu_ctx.fir_block_f16_dev(xh, n, nstreams, n, d_h, ntaps, sth, ns, y, n)
+        xs_ = (n + 7) // 8 * 8  # fp16 rows 16-B aligned (the call's precondition with several streams)
+        xp = np.zeros((nstreams, xs_), np.float16)
+        xp[:, :n] = x.astype(np.float16)
+        xh = sdrhip.DeviceArray.from_numpy(gpu_ctx, xp)
+        gpu_ctx.fir_block_f16_dev(xh, n, nstreams, xs_, d_h, ntaps, sth, ns, y, n)
         gpu_ctx.synchronize()
         got = y.download().reshape(nstreams, n)
         for s in range(nstreams):
@@ -1080,3 +1086,20 @@ def test_batched_random_shapes(gpu_ctx, oracle, built_lib, D, ntaps, ns, n, nstr
         assert_bits(d_sq.download().reshape(nstreams, ns), np.stack([o["sq"] for o in ors]), f"state_q block {b}")
         assert_bits(d_pi.download(), np.array([o["prev"][0] for o in ors], np.float32), f"prev_i block {b}")
         assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), f"prev_q block {b}")
+
+
+_F16 = []
+for _ in range(10):
+    _T = int(_RNG.choice([8 * int(_RNG.integers(1, 257)), int(_RNG.integers(2, 600))]))
+    _F16.append((_T, int(_RNG.integers(max(_T, 8), 40000)), int(_RNG.integers(1, 4))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["mfma", "dot2"])
+@pytest.mark.parametrize("ntaps,n,nstreams", _F16, ids=[f"T{t}-n{n}-S{k}" for t, n, k in _F16])
+def test_fir_block_f16_random_shapes(gpu_ctx, oracle, built_lib, kswitch, ntaps, n, nstreams, kernel):
+    """The fp16 arm's tolerance contract (as test_fir_block_f16_tolerance) on
+    seeded random shapes: tap counts on and off the MFMA kernel's T % 8 grid,
+    1-3 streams, blocks from the tap count to 40 k."""
+    kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
+    _f16_tolerance_check(gpu_ctx, oracle, built_lib, ntaps, n, nstreams, ntaps * 7 + n)
