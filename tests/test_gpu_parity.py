@@ -1103,3 +1103,46 @@ def test_fir_block_f16_random_shapes(gpu_ctx, oracle, built_lib, kswitch, ntaps,
     1-3 streams, blocks from the tap count to 40 k."""
     kswitch("SDR_F16_MFMA", "1" if kernel == "mfma" else "0")
     _f16_tolerance_check(gpu_ctx, oracle, built_lib, ntaps, n, nstreams, ntaps * 7 + n)
+
+
+_RESB = []
+for _ in range(8):
+    _up = int(_RNG.choice([int(_RNG.integers(1, 12)), int(_RNG.integers(12, 449))]))
+    _down = int(_RNG.choice([4 * int(_RNG.integers(1, 330)), int(_RNG.integers(1, 1300))]))
+    _cnt = int(_RNG.choice([101, 151, int(_RNG.integers(2, 60))]))
+    _ns = _cnt - 1 + int(_RNG.integers(0, 8))
+    _q = _down // math.gcd(_up, _down)
+    _n = _q * max(1, int(_RNG.integers(1, 9000)) // _q)
+    _n = max(_n, (_ns + _q - 1) // _q * _q)
+    _RESB.append((_up, _down, _cnt, _ns, _n, int(_RNG.integers(1, 6)), int(_RNG.integers(0, 5))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", list(RESAMPLE_KERNELS))
+@pytest.mark.parametrize("up,down,cnt,ns,n,nstreams,xpad", _RESB,
+                         ids=[f"L{u}-M{d}-C{c}-ns{s}-n{n}-S{k}-px{p}" for u, d, c, s, n, k, p in _RESB])
+def test_resample_batched_random_shapes(gpu_ctx, oracle, built_lib, kswitch, kernel, up, down, cnt, ns, n,
+                                        nstreams, xpad):
+    """The batched resampler on seeded random shapes (T = cnt * up, lane-phase
+    shapes and others, padded input rows) under every kernel setting, three
+    blocks, every stream and state bitwise against the oracle."""
+    for k, v in RESAMPLE_KERNELS[kernel].items():
+        kswitch(k, v)
+    sdrhip = built_lib
+    rng = np.random.default_rng(up * 1009 + down * 7 + cnt + n)
+    h = (rng.standard_normal(cnt * up) / cnt).astype(np.float32)
+    ny = sdrhip.resample_out_len(up, down, n)
+    states = [rng.standard_normal(ns).astype(np.float32) for _ in range(nstreams)]
+    d_h = sdrhip.DeviceArray.from_numpy(gpu_ctx, h)
+    d_st = sdrhip.DeviceArray.from_numpy(gpu_ctx, np.stack(states))
+    xs, ys = n + xpad, ny + 1
+    d_y = sdrhip.DeviceArray(gpu_ctx, nstreams * ys * 4)
+    for blk in range(3):
+        x = rng.standard_normal((nstreams, xs)).astype(np.float32)
+        d_x = sdrhip.DeviceArray.from_numpy(gpu_ctx, x)
+        gpu_ctx.resample_dev(up, down, d_x, n, nstreams, xs, d_h, len(h), d_st, ns, d_y, ys)
+        gpu_ctx.synchronize()
+        got = d_y.download().reshape(nstreams, ys)[:, :ny]
+        for s in range(nstreams):
+            assert_bits(got[s], oracle.resample(up, down, x[s, :n], h, states[s]), f"stream {s} block {blk}")
+        assert_bits(d_st.download().reshape(nstreams, ns), np.stack(states), f"state block {blk}")
