@@ -346,3 +346,54 @@ def test_device_stereo_pipeline(gpu_ctx, oracle, built_lib, mode, api):
         for s in range(nstreams):
             assert_bits(prev[s], ost[s]["prev"], f"prev stream {s} block {b}")
 
+
+
+_MRNG = np.random.default_rng(20261019)
+_MONO_RANDOM = []
+for _ in range(8):
+    _mode = int(_MRNG.choice([0, 1]))
+    _D, _down = MODES[_mode][1], MODES[_mode][4]
+    _k = int(_MRNG.integers(120 // _down + 1, 1200))  # audio block >= its 100-sample state
+    # wire rows 8-B aligned (the fused layout) or not (the separate launches);
+    # nd stays a multiple of down (the reference's own precondition, refused otherwise)
+    _pad = int(_MRNG.choice([0, 8])) if _MRNG.integers(0, 2) else int(_MRNG.choice([3, 5]))
+    _MONO_RANDOM.append((_mode, _D * _k * _down, int(_MRNG.integers(1, 6)), _pad))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,npairs,nstreams,pad", _MONO_RANDOM,
+                         ids=[f"m{m}-n{n}-S{k}-pad{p}" for m, n, k, p in _MONO_RANDOM])
+def test_device_mono_random_blocks(gpu_ctx, oracle, built_lib, mode, npairs, nstreams, pad):
+    """sdr_mono_pcm_u8_dev on seeded random block lengths (modes 0 and 1's
+    filters, 1-5 streams, wire rows aligned or not), three blocks: PCM bytes equal to the
+    oracle chain block by block.  (Aligned rows: the fused layout at up == 1;
+    misaligned: the generic front end and separate launches.)"""
+    sdrhip = built_lib
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, D, up, down, _, h_rf, h_audio = _mono_setup(oracle, mode)
+    nblk, nb = 3, 2 * npairs
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    streams = [fm_iq_u8(npairs * nblk, seed=500 + 11 * s + npairs, fs=rf_fs) for s in range(nstreams)]
+    A = sdrhip.DeviceArray
+    d_hrf, d_ha = A.from_numpy(gpu_ctx, h_rf), A.from_numpy(gpu_ctx, h_audio)
+    z = lambda k: A.from_numpy(gpu_ctx, np.zeros(nstreams * k, np.float32))  # noqa: E731
+    si, sq, pi, pq, sd, sa = z(100), z(100), z(1), z(1), z(50), z(100)
+    ost = [dict(i=np.zeros(100, np.float32), q=np.zeros(100, np.float32), prev=np.zeros(2, np.float32),
+                delay=np.zeros(50, np.float32), audio=np.zeros(100, np.float32)) for _ in range(nstreams)]
+    pcm_stride = na + 3
+    d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
+    for b in range(nblk):
+        blk = np.zeros((nstreams, nb + pad), np.uint8)
+        for s in range(nstreams):
+            blk[s, :nb] = streams[s][b * nb:(b + 1) * nb]
+        d_iq = A.from_numpy(gpu_ctx, blk)
+        gpu_ctx.mono_pcm_u8_dev(D, d_iq, npairs, nstreams, nb + pad, d_hrf, len(h_rf), si, sq, 100, pi, pq,
+                                sd, 50, up, down, d_ha, len(h_audio), sa, 100, d_pcm, pcm_stride)
+        gpu_ctx.synchronize()
+        out = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :na]
+        for s in range(nstreams):
+            st = ost[s]
+            want = oracle.mono(D, blk[s, :nb], h_rf, st["i"], st["q"], st["prev"], st["delay"], up, down, h_audio,
+                               st["audio"])
+            assert np.array_equal(out[s], want), f"stream {s} block {b}"
