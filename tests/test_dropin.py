@@ -397,3 +397,67 @@ def test_device_mono_random_blocks(gpu_ctx, oracle, built_lib, mode, npairs, nst
             want = oracle.mono(D, blk[s, :nb], h_rf, st["i"], st["q"], st["prev"], st["delay"], up, down, h_audio,
                                st["audio"])
             assert np.array_equal(out[s], want), f"stream {s} block {b}"
+
+
+_STEREO_RANDOM = []
+for _ in range(6):
+    _mode = int(_MRNG.choice([0, 1]))
+    _D, _down = MODES[_mode][1], MODES[_mode][4]
+    _k = int(_MRNG.integers(120 // _down + 1, 1500))
+    _STEREO_RANDOM.append((_mode, _D * _k * _down, int(_MRNG.integers(1, 5)), str(_MRNG.choice(["one", "split"]))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,npairs,nstreams,api", _STEREO_RANDOM,
+                         ids=[f"m{m}-n{n}-S{k}-{a}" for m, n, k, a in _STEREO_RANDOM])
+def test_device_stereo_random_blocks(gpu_ctx, oracle, built_lib, mode, npairs, nstreams, api):
+    """The device stereo program on seeded random block lengths (modes 0 and
+    1, 1-4 streams, one call or the two-stage split): PCM bytes and every
+    carried state, the PLL's six floats included, equal to the oracle chain
+    after each of three blocks -- block lengths off the PLL's 8-sample chunk
+    grid included."""
+    sdrhip = built_lib
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, D, audio_fs, up, down, _, taps = _stereo_setup(oracle, mode)
+    nblk, nb = 3, 2 * npairs
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    streams = [fm_iq_u8(npairs * nblk, seed=700 + 13 * s + npairs, fs=rf_fs) for s in range(nstreams)]
+    A = sdrhip.DeviceArray
+    d_taps = {k: A.from_numpy(gpu_ctx, v) for k, v in taps.items()}
+    t = sdrhip.StereoTaps(d_taps["rf"].ptr, 101, d_taps["audio"].ptr, len(taps["audio"]), d_taps["pilot"].ptr,
+                          d_taps["stereo"].ptr, 101)
+    st0 = _stereo_state0()
+    d_st = {k: A.from_numpy(gpu_ctx, np.tile(v, nstreams)) for k, v in st0.items() if k != "prev"}
+    d_pi = A.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    d_pq = A.from_numpy(gpu_ctx, np.zeros(nstreams, np.float32))
+    state = sdrhip.StereoState(d_st["i"].ptr, d_st["q"].ptr, 100, d_pi.ptr, d_pq.ptr, d_st["delay"].ptr, 50,
+                               d_st["audio"].ptr, d_st["stereo_lp"].ptr, 100, d_st["pilot"].ptr, d_st["stereo"].ptr,
+                               100, d_st["pll"].ptr)
+    pcm_stride = 2 * na + 2
+    d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
+    ost = [_stereo_state0() for _ in range(nstreams)]
+    work = gpu_ctx.stereo_work(D, npairs, up, down, nstreams) if api == "split" else None
+    try:
+        for b in range(nblk):
+            blk = np.stack([streams[s][b * nb:(b + 1) * nb] for s in range(nstreams)])
+            d_iq = A.from_numpy(gpu_ctx, blk)
+            if work is None:
+                gpu_ctx.stereo_pcm_u8_dev(D, d_iq, npairs, nstreams, nb, up, down, audio_fs, t, state, d_pcm,
+                                          pcm_stride)
+            else:
+                gpu_ctx.stereo_front_u8_dev(d_iq, nb, t, state, work)
+                gpu_ctx.stereo_back_dev(audio_fs, t, state, work, d_pcm, pcm_stride)
+            gpu_ctx.synchronize()
+            got = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :2 * na]
+            for s in range(nstreams):
+                want = oracle.stereo(D, blk[s], taps["rf"], ost[s], up, down, taps["audio"], taps["pilot"],
+                                     taps["stereo"], audio_fs)
+                assert np.array_equal(got[s], want), f"stream {s} block {b}"
+            for k in ("pll", "pilot", "stereo", "stereo_lp", "audio", "delay"):
+                dev = d_st[k].download().reshape(nstreams, -1)
+                for s in range(nstreams):
+                    assert_bits(dev[s], ost[s][k], f"{k} stream {s} block {b}")
+    finally:
+        if work is not None:
+            work.close()
