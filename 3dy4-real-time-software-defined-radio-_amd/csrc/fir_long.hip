@@ -581,16 +581,23 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   constexpr int G = kMfG;
   const int ngrp = SDR_ABL(a.ablate) == 2 ? 0 : a.kd / (16 * G);  // (ablation 2: no MFMA)
   half8 av[G], bv[G][kMfNT];
-  auto fetch = [&](int g0, half8 (&aa)[G], half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
+  // B's fragment of step s, tile t sits at padded index mf_pad(b + 16 s +
+  // 1024 t), b = tb0 + 32 i + 8 hh; since 8 hh < 32 that is mf_pad(b) + 16 s
+  // + 8 (s >> 1) + 1280 t.  The loop walks both operands from pointers that
+  // advance once per pair of groups (2 G steps: A 32 G halves, B 40 G), so
+  // every read in the body is one ds_read_b128 at an immediate offset -- no
+  // per-read address arithmetic (mf_pad of a run-time step index cost ~4
+  // VALU per B read)
+  const _Float16* brow = img + mf_pad(tb0 + 32 * i + 8 * hh);
+  auto fetch = [&](const _Float16* ap, const _Float16* bp, int par, half8 (&aa)[G], half8 (&bb)[G][kMfNT])
+      __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-      const int sidx = g0 * G + u;
-      aa[u] = *reinterpret_cast<const half8*>(arow + 16 * sidx);
+      const int st = par * G + u;  // step within the pair of groups (a constant once inlined)
+      aa[u] = *reinterpret_cast<const half8*>(ap + 16 * st);
 #pragma unroll
-      for (int t = 0; t < kMfNT; ++t) {
-        const int p = tb0 + t * 1024 + 32 * i + 16 * sidx + 8 * hh;  // image index of B's fragment
-        bb[u][t] = *reinterpret_cast<const half8*>(img + mf_pad(p));
-      }
+      for (int t = 0; t < kMfNT; ++t)
+        bb[u][t] = *reinterpret_cast<const half8*>(bp + 1280 * t + 16 * st + 8 * (st >> 1));
     }
   };
   auto mfmas = [&](const half8 (&aa)[G], const half8 (&bb)[G][kMfNT]) __attribute__((always_inline)) {
@@ -601,11 +608,15 @@ __global__ __launch_bounds__(64 * kMfWaves) void fir_long_mfma(MfArgs a) {
   };
   // two register sets in ping-pong (ngrp is even): no copies between groups
   half8 an[G], bn[G][kMfNT];
-  fetch(0, av, bv);
+  const _Float16* ap = arow;
+  const _Float16* bp = brow;
+  fetch(ap, bp, 0, av, bv);
   for (int g = 0; g < ngrp; g += 2) {
-    fetch(g + 1, an, bn);
+    fetch(ap, bp, 1, an, bn);
     mfmas(av, bv);
-    if (g + 2 < ngrp) fetch(g + 2, av, bv);
+    ap += 32 * G;
+    bp += 40 * G;
+    if (g + 2 < ngrp) fetch(ap, bp, 0, av, bv);
     mfmas(an, bn);
   }
 #ifdef SDR_TIMING_BUILD
