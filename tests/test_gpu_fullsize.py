@@ -1,20 +1,23 @@
 """GPU parity at BASELINE.json's full sizes, through the exact launches the
 benchmark times (f32 planar `frontend_dev`, state carried across steps):
 
-* config 2: 1,024 streams x 65,540 pairs, two consecutive steps -- sampled
-  streams against the oracle bit for bit, and EVERY stream's carried state
-  (state_i/q = the block's last 100 inputs; prev_i/q = its last decimated
-  I/Q, recomputed in numpy in the reference's fp32 order) bit for bit;
+* config 2: 1,024 streams x 65,540 pairs, two consecutive steps -- EVERY
+  stream's outputs against the oracle bit for bit (the oracle threaded over
+  streams), and every stream's carried state (state_i/q = the block's last
+  100 inputs; prev_i/q = its last decimated I/Q, recomputed in numpy in the
+  reference's fp32 order) bit for bit;
 * config 2 under SDR_ARITH_FMA: every stream within the SURVEY 8(d) bar of
   the exact path;
 * config 4: 262,150-pair blocks (2 consecutive, 3 streams), one stream as a
-  single 8,388,800-pair call (the bench's cfg4x8 per-stream call) and as a
-  single 67,110,400-pair call (the bench's cfg4 launch), each against the
-  oracle run block by block -- block-size independence, src/filter.cpp:139;
-* config 5: the 1024-tap FIR over 2 x 1,048,576 samples, windows at the
-  start (real state), middle and end checked against the oracle (each
-  window's state is the preceding 1,023 inputs, src/filter.cpp:82); its
-  fp16 arm over the whole 2 x 1,048,576 within the stated tolerance;
+  single 8,388,800-pair call, the bench's cfg4x8 launch (8 streams x
+  8,388,800 pairs in ONE batched call) and the bench's cfg4 launch (one
+  stream x 67,110,400 pairs in one call), each against the oracle run block
+  by block -- block-size independence, src/filter.cpp:139;
+* config 5: the 1024-tap FIR over 2 x 1,048,576 samples, EVERY output
+  against the oracle: the first window from the real state, every later
+  window seeded with the 1,023 inputs before it (src/filter.cpp:82), the
+  windows threaded; its fp16 arm over the whole 2 x 1,048,576 within the
+  stated tolerance;
 * config 3: the resampler plan at the bench's launch (1,024 x 65,600, the
   real 22,197-tap design), two steps, every stream bitwise.
 """
@@ -62,7 +65,8 @@ def _planar_batch(sdrhip, ctx, nstreams, n, seed, stride=None):
 
 @pytest.mark.parametrize("kernel", ["tile", "sc"])
 def test_cfg2_full_f32_two_steps(gpu_ctx, oracle, built_lib, kswitch, kernel):
-    """kernel: fir_tile, or fir_tile_sc (SDR_FIR_SC=1); the bench's launches either way."""
+    """kernel: fir_tile, or fir_tile_sc (SDR_FIR_SC=1); the bench's launch
+    either way.  All 1,024 streams' outputs and states, both steps."""
     kswitch("SDR_FIR_SC", "0" if kernel == "tile" else "1")
     sdrhip = built_lib
     S, n, D = 1024, 65540, 10
@@ -72,23 +76,29 @@ def test_cfg2_full_f32_two_steps(gpu_ctx, oracle, built_lib, kswitch, kernel):
     d_si, d_sq = _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32)), _dev(sdrhip, gpu_ctx, np.zeros((S, 100), np.float32))
     d_pi, d_pq = _dev(sdrhip, gpu_ctx, _z(S)), _dev(sdrhip, gpu_ctx, _z(S))
     d_out = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
-    sample = (0, 1, 2, 255, 511, 700, 1022, 1023)
-    ors = {s: dict(si=_z(100), sq=_z(100), prev=_z(2)) for s in sample}
+    ors = [dict(si=_z(100), sq=_z(100), prev=_z(2)) for _ in range(S)]
     for step, seed in enumerate((301, 302)):
         d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, seed)
+        d_out.fill(0xFF)
         gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
         gpu_ctx.synchronize()
         got = d_out.download().reshape(S, nout)
         I = d_I.download().reshape(S, n)
         Q = d_Q.download().reshape(S, n)
-        for s in sample:
-            want = oracle.frontend(D, I[s], Q[s], h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"])
-            assert_bits(got[s], want, f"step {step} stream {s}")
-        # every stream's carried state
+        with cf.ThreadPoolExecutor(16) as ex:  # C behind ctypes: the GIL is released
+            want = np.stack(list(ex.map(
+                lambda s: oracle.frontend(D, I[s], Q[s], h, ors[s]["si"], ors[s]["sq"], ors[s]["prev"]), range(S))))
+        assert_bits(got, want, f"step {step}: all {S} streams")
+        # every stream's carried state, against the oracle and against the
+        # reference's rule restated in numpy
+        assert_bits(d_si.download().reshape(S, 100), np.stack([o["si"] for o in ors]), f"step {step} state_i")
+        assert_bits(d_sq.download().reshape(S, 100), np.stack([o["sq"] for o in ors]), f"step {step} state_q")
         assert_bits(d_si.download().reshape(S, 100), I[:, n - 100:], f"step {step} state_i (all streams)")
         assert_bits(d_sq.download().reshape(S, 100), Q[:, n - 100:], f"step {step} state_q (all streams)")
         assert_bits(d_pi.download(), _last_output(h, I, D), f"step {step} prev_i (all streams)")
         assert_bits(d_pq.download(), _last_output(h, Q, D), f"step {step} prev_q (all streams)")
+        assert_bits(d_pi.download(), np.array([o["prev"][0] for o in ors], np.float32), f"step {step} prev_i")
+        assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), f"step {step} prev_q")
         assert np.isfinite(got).all()
         d_I.free()
         d_Q.free()
@@ -193,6 +203,50 @@ def test_cfg4_single_call_equals_blocks(gpu_ctx, oracle, built_lib):
     assert_bits(np.concatenate([d_pi.download(), d_pq.download()]), pv, "prev")
 
 
+def test_cfg4x8_full_call(gpu_ctx, oracle, built_lib):
+    """bench.py's cfg4x8 launch exactly: 8 independent streams x 8,388,800
+    pairs (32 x 262,150) in ONE batched frontend_dev call, each stream with its
+    own non-zero carried state, against the oracle run block by block over the
+    same samples (src/filter.cpp:139): every output and every state bitwise."""
+    sdrhip = built_lib
+    S, nblk, blk, D = 8, 32, 262150, 10
+    n = nblk * blk
+    nout, nb = n // D, blk // D
+    h = load_golden("taps")["lpf_rf_mode0"]
+    d_h = _dev(sdrhip, gpu_ctx, h)
+    d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, S, n, 4848)
+    st0 = np.random.default_rng(8).uniform(-0.7, 0.7, (2, S, 100)).astype(np.float32)
+    pv0 = np.random.default_rng(9).uniform(-0.7, 0.7, (2, S)).astype(np.float32)
+    d_si, d_sq = _dev(sdrhip, gpu_ctx, st0[0]), _dev(sdrhip, gpu_ctx, st0[1])
+    d_pi, d_pq = _dev(sdrhip, gpu_ctx, pv0[0]), _dev(sdrhip, gpu_ctx, pv0[1])
+    d_out = sdrhip.DeviceArray(gpu_ctx, S * nout * 4)
+    d_out.fill(0xFF)
+    gpu_ctx.frontend_dev(D, d_I, d_Q, n, S, n, d_h, 101, d_si, d_sq, 100, d_pi, d_pq, d_out, nout)
+    gpu_ctx.synchronize()
+    got = d_out.download().reshape(S, nout)
+    I, Q = d_I.download().reshape(S, n), d_Q.download().reshape(S, n)
+    d_I.free()
+    d_Q.free()
+    ors = [dict(si=st0[0, s].copy(), sq=st0[1, s].copy(), prev=np.array([pv0[0, s], pv0[1, s]], np.float32))
+           for s in range(S)]
+
+    def run(s):
+        o = ors[s]
+        return np.concatenate([oracle.frontend(D, I[s, b * blk:(b + 1) * blk], Q[s, b * blk:(b + 1) * blk], h,
+                                               o["si"], o["sq"], o["prev"]) for b in range(nblk)])
+
+    with cf.ThreadPoolExecutor(S) as ex:
+        want = list(ex.map(run, range(S)))
+    for s in range(S):
+        for b in range(0, nblk, 8):  # report a failing stream by its 8-block span
+            assert_bits(got[s, b * nb:(b + 8) * nb], want[s][b * nb:(b + 8) * nb], f"stream {s} blocks {b}..{b + 7}")
+    assert_bits(d_si.download().reshape(S, 100), np.stack([o["si"] for o in ors]), "state_i")
+    assert_bits(d_sq.download().reshape(S, 100), np.stack([o["sq"] for o in ors]), "state_q")
+    assert_bits(d_pi.download(), np.array([o["prev"][0] for o in ors], np.float32), "prev_i")
+    assert_bits(d_pq.download(), np.array([o["prev"][1] for o in ors], np.float32), "prev_q")
+    assert np.isfinite(got).all()
+
+
 def test_cfg4_full_single_call(gpu_ctx, oracle, built_lib):
     """bench.py's cfg4 launch exactly: ONE stream x 67,110,400 pairs (256 x
     262,150) in a single frontend_dev call -- about 53 k tiles of one stream
@@ -229,10 +283,13 @@ def test_cfg4_full_single_call(gpu_ctx, oracle, built_lib):
 
 def test_cfg5_full_windows(gpu_ctx, oracle, built_lib):
     """BASELINE config 5 at full size: 2 x 1,048,576 samples through the exact
-    1024-tap FIR; windows checked against the oracle (any window equals a
-    block-by-block run whose state is the 1,023 inputs before it)."""
+    1024-tap FIR, EVERY output against the oracle.  The record is cut into
+    65,536-sample windows run in parallel: the first from the real carried
+    state, each later one seeded with the 1,023 inputs before it -- the
+    reference's own block rule (src/filter.cpp:82) makes that window equal to
+    the same samples of one whole-record call."""
     sdrhip = built_lib
-    n, T, W = 1048576, 1024, 4096
+    n, T, W = 1048576, 1024, 65536
     h = oracle.taps_lpf(2.4e6, 100e3, T, 1)
     d_h = _dev(sdrhip, gpu_ctx, h)
     d_I, d_Q = _planar_batch(sdrhip, gpu_ctx, 1, n, 55)
@@ -240,15 +297,21 @@ def test_cfg5_full_windows(gpu_ctx, oracle, built_lib):
     st0 = np.random.default_rng(4).uniform(-0.7, 0.7, (2, T - 1)).astype(np.float32)
     d_x, d_st = _dev(sdrhip, gpu_ctx, x), _dev(sdrhip, gpu_ctx, st0)
     d_y = sdrhip.DeviceArray(gpu_ctx, 2 * n * 4)
+    d_y.fill(0xFF)
     gpu_ctx.fir_block_dev(d_x, n, 2, n, d_h, T, d_st, T - 1, d_y, n)
     gpu_ctx.synchronize()
     y = d_y.download().reshape(2, n)
-    for c in range(2):
-        want0 = oracle.fir_block(x[c, :W], h, st0[c].copy())
-        assert_bits(y[c, :W], want0, f"channel {c} first window")
-        for a in (n // 2 + 13, n - W):
-            want = oracle.fir_block(x[c, a:a + W], h, x[c, a - (T - 1):a].copy())
-            assert_bits(y[c, a:a + W], want, f"channel {c} window at {a}")
+
+    def window(job):
+        c, a = job
+        st = st0[c].copy() if a == 0 else x[c, a - (T - 1):a].copy()
+        return oracle.fir_block(x[c, a:a + W], h, st)
+
+    jobs = [(c, a) for c in range(2) for a in range(0, n, W)]
+    with cf.ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(window, jobs))
+    for (c, a), w in zip(jobs, want):
+        assert_bits(y[c, a:a + W], w, f"channel {c} window at {a}")
     assert_bits(d_st.download().reshape(2, T - 1), x[:, n - (T - 1):], "state")
 
 
