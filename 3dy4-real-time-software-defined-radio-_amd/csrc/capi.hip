@@ -1474,4 +1474,45 @@ int sdr_frontend_u8(sdr_ctx* c, int D, const uint8_t* iq, long long npairs, cons
                        prev_q, demod);
 }
 
+// ------------------------------------------ device transcendental routines --
+int sdr_libm_sincos_hash_dev(sdr_ctx* c, int mode, unsigned chunk_lo, unsigned chunk_hi, unsigned long long* hash) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!hash || (mode != 0 && mode != 1) || chunk_hi > 4096u || chunk_lo >= chunk_hi)
+    return fail(c, SDR_EINVAL, "libm sincos hash: mode %d, chunks [%u, %u) of 4096", mode, chunk_lo, chunk_hi);
+  SDR_HIP(c, sdr::launch_libm_sincos_hash(mode, chunk_lo, chunk_hi - chunk_lo, hash, c->cur));
+  return SDR_OK;
+}
+
+int sdr_libm_sincos_diff_dev(sdr_ctx* c, unsigned chunk_lo, unsigned chunk_hi, unsigned long long* count,
+                             unsigned* args, long long cap) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!count || !args || cap < 0 || chunk_hi > 4096u || chunk_lo >= chunk_hi)
+    return fail(c, SDR_EINVAL, "libm sincos diff: chunks [%u, %u) of 4096, cap %lld", chunk_lo, chunk_hi, cap);
+  SDR_HIP(c, sdr::launch_libm_sincos_diff(chunk_lo, chunk_hi - chunk_lo, count, args, cap, c->cur));
+  return SDR_OK;
+}
+
+int sdr_libm_eval_dev(sdr_ctx* c, int fn, const float* a, const float* b, long long n, float* out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!a || !out || fn < 0 || fn > 5 || ((fn == 2 || fn == 5) && !b) || n < 0)
+    return fail(c, SDR_EINVAL, "libm eval: fn %d, n %lld", fn, n);
+  if (n == 0) return SDR_OK;
+  SDR_HIP(c, sdr::launch_libm_eval(fn, a, b, n, out, c->cur));
+  return SDR_OK;
+}
+
+int sdr_libm_atan2_screen_dev(sdr_ctx* c, unsigned long long seed, unsigned long long first, unsigned long long count,
+                              unsigned* cand, long long cand_cap, unsigned* out, long long out_cap,
+                              unsigned long long* counters) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!cand || !out || !counters || cand_cap < 1 || out_cap < 0 || count == 0 || count > (1ull << 32))
+    return fail(c, SDR_EINVAL, "libm atan2 screen: count %llu (1 .. 2^32), cand_cap %lld", count, cand_cap);
+  SDR_HIP(c, sdr::launch_libm_atan2_screen(seed, first, count, cand, cand_cap, out, out_cap, counters, c->cur));
+  return SDR_OK;
+}
+
 }  // extern "C"

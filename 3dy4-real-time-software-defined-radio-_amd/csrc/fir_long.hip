@@ -716,9 +716,11 @@ __global__ __launch_bounds__(kWG) void f32_to_f16(const float* __restrict__ x, l
 
 }  // namespace
 
-// T <= 4096: the image, tap copies and reversed taps fit the LDS (about
-// 106 KiB at 4096), and no workgroup but a stream's first reaches into the
-// state (T < kMfOut), which lets that one commit the new state in-kernel
+// T <= 4096: the image, tap copies, reversed taps and one output transpose
+// area per wave fit the LDS (at 4096: 123 KiB with 4 waves, 141 KiB with 8;
+// at 1024: 61 / 79 KiB; launch_fir_long_h checks the CU's LDS), and no
+// workgroup but a stream's first reaches into the state (T < kMfOut), which
+// lets that one commit the new state in-kernel
 bool fir_f16_uses_mfma(int ntaps) {
   return ntaps % 8 == 0 && ntaps <= 4096 && sw(kSwF16Mfma) != 0;
 }
@@ -802,18 +804,19 @@ hipError_t launch_fir_long_h(const void* x, long long n, int nstreams, long long
     static const int tr = SDR_TIMING_ENV("SDR_F16_TRACE", 0);
     if (tr) a.trace = mf_trace_buffer((size_t)a.wg_per_stream * nstreams * kMfTraceW);
 #endif
-    // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves),
-    // (SDR_F16_TSTORE) one output transpose area per wave
-    const size_t taps_end = (size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40);
-    a.ost = (int)((taps_end + 7) / 8 * 8);
-    const size_t lds = (SDR_F16_TSTORE ? (size_t)a.ost * sizeof(_Float16) + 8 * 32 * kMfOstRow * sizeof(float)
-                                       : taps_end * sizeof(_Float16));
-    const long long blocks = (long long)a.wg_per_stream * nstreams;
-    if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
     // one launch: each stream's first workgroup commits the state itself
     // two waves per SIMD, one tile each: 8.8 vs 10.9 us per kernel on cfg5h
     // (profiles/r04y/); SDR_F16_W8=0 restores four waves of two tiles
     const int w8 = sw(kSwF16W8);
+    // image, 8 tap copies, (no plan) the reversed taps (a.lc + 40 halves),
+    // (SDR_F16_TSTORE) one output transpose area per wave of the variant
+    const size_t taps_end = (size_t)mf_pad(a.span) + 8 + (plan ? 8 : 9) * (size_t)a.lc + (plan ? 0 : 40);
+    a.ost = (int)((taps_end + 7) / 8 * 8);
+    const size_t waves = w8 ? 8 : 4;
+    const size_t lds = (SDR_F16_TSTORE ? (size_t)a.ost * sizeof(_Float16) + waves * 32 * kMfOstRow * sizeof(float)
+                                       : taps_end * sizeof(_Float16));
+    const long long blocks = (long long)a.wg_per_stream * nstreams;
+    if (blocks > 0x7fffffffLL || lds > (size_t)device_lds_bytes()) return hipErrorInvalidValue;
     if (w8 && plan)
       hipLaunchKernelGGL((fir_long_mfma<8, true>), dim3((unsigned)blocks), dim3(512), lds, st, a);
     else if (w8)

@@ -207,4 +207,14 @@ bool launch_resample_rs(int up, int down, const float* x, long long n, int nstre
 bool resample_lp_tables(int up, int down, const float* h, int ntaps, int ns, float* tables, hipStream_t st,
                         hipError_t* err);
 
+// libm_check.hip: the device transcendental routines in bulk (parity tests)
+hipError_t launch_libm_sincos_hash(int mode, unsigned chunk_lo, unsigned nchunks, unsigned long long* hash,
+                                   hipStream_t st);
+hipError_t launch_libm_sincos_diff(unsigned chunk_lo, unsigned nchunks, unsigned long long* count, unsigned* args,
+                                   long long cap, hipStream_t st);
+hipError_t launch_libm_eval(int fn, const float* a, const float* b, long long n, float* out, hipStream_t st);
+hipError_t launch_libm_atan2_screen(unsigned long long seed, unsigned long long first, unsigned long long count,
+                                    unsigned* cand, long long cand_cap, unsigned* out, long long out_cap,
+                                    unsigned long long* counters, hipStream_t st);
+
 }  // namespace sdr

@@ -12,11 +12,14 @@
 // does not feed back, is evaluated afterwards in parallel over samples.
 // Arithmetic follows the reference's promotions exactly: the loop filter in
 // fp32, atan2 / cos / sin of the fp32
-// arguments in double (the reference calls the double C functions), every
-// result rounded back to float where the reference stores a float.
+// arguments as glibc's double routines give them (the reference calls the
+// double C functions), every result rounded back to float where the reference
+// stores a float: libm_exact.hpp, proved over every fp32 argument of sin / cos
+// against glibc (tests/test_libm_exact.py).
 #include <type_traits>
 
 #include "sdr_common.hpp"
+#include "libm_exact.hpp"
 #include "pll_fast.hpp"
 
 #pragma clang fp contract(off)
@@ -25,6 +28,44 @@ namespace sdr {
 namespace {
 
 constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
+
+constexpr int kPllChunk = 8;
+struct PllState {
+  float fbI, fbQ, integrator, phaseEst, trigOffset, arg;
+};
+struct PllChunk {
+  float v[kPllChunk];
+};
+// One step of the recurrence (src/filter.cpp:188-219) with libm_exact.hpp's
+// routines: glibc's floats for every argument.
+__device__ __forceinline__ void pll_exact_step(PllState& p, float v, float Kp, float Ki, double step) {
+  const float eI = (v == 0.0f ? 1.0f : v) * p.fbI;
+  const float eQ = v * (-1.0f * p.fbQ);
+  const float eD = libmx::atan2_f(eQ, eI);
+  p.integrator = p.integrator + Ki * eD;
+  p.phaseEst = p.phaseEst + (Kp * eD + p.integrator);
+  p.trigOffset = p.trigOffset + 1.0f;
+  p.arg = (float)(step * (double)p.trigOffset + (double)p.phaseEst);
+  const libmx::SinCos sc = libmx::sincos_f(p.arg);  // glibc's sincos (the reference's -O3 build fuses cos + sin)
+  p.fbI = sc.c;
+  p.fbQ = sc.s;
+}
+// An uncertified chunk's exact re-run (steps k0 .. k0+m-1, arguments to
+// ar[k0+1 ..]), out of line: it is rare, and inlined it shares the hot loop's
+// register allocation (pll_kernel 1,055 vs 946 us per stereo0 block,
+// profiles/r06d/, r06e/).
+__device__ __attribute__((noinline)) PllState pll_exact_chunk(PllState p, PllChunk c, int m, float Kp, float Ki,
+                                                              double step, float* ar, long long k0, long long n) {
+#pragma unroll
+  for (int j = 0; j < kPllChunk; ++j) {
+    if (j < m) {
+      pll_exact_step(p, c.v[j], Kp, Ki, step);
+      if (k0 + j + 1 < n) ar[k0 + j + 1] = p.arg;
+    }
+  }
+  return p;
+}
+
 
 // pll[6] per stream: feedbackI, feedbackQ, integrator, phaseEst, trigOffset, nco_state
 // (src/project.cpp:48-55).  Only the recurrence runs here: the phase detector
@@ -37,10 +78,10 @@ constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
 // FAST: each step first runs the short-chain atan2 / sincos of pll_fast.hpp,
 // which certify that their float results are the reference's; a chunk of 8
 // steps in which any lane of the wave could not certify a result is run again
-// from its saved state with the library routines (a wave-uniform branch, off
-// the recurrence's chain).  The stored arguments of the first pass are
-// rewritten by the second, so every output is the library path's or a
-// certified equal.
+// from its saved state with libm_exact.hpp's routines (a wave-uniform branch,
+// off the recurrence's chain), which give glibc's floats.  The stored
+// arguments of the first pass are rewritten by the second, so every output is
+// the exact path's or a certified equal.
 //
 // GUARD: where a chunk's input check (pllfast::input_ok on its 8 samples)
 // comes from -- 0: evaluated in the kernel, 1: guard[s * nchunk + c], written
@@ -48,7 +89,6 @@ constexpr double kPiD = 3.14159265358979323846;  // include/dy4.h:14
 // check is off the recurrence's dependency chain, but the one wave per SIMD
 // issues every instruction itself: in the kernel it cost 7.6 % of stereo0
 // (profiles/r03_ab/pll_guard.txt).
-constexpr int kPllChunk = 8;
 template <int FAST, int GUARD>
 __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, long long n, int nstreams,
                                                  long long in_stride, float freq, float Fs, float nco_scale,
@@ -67,19 +107,19 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
   const float Ki = norm_bw * norm_bw * 3.555f;
   const double step = 2.0 * kPiD * (double)(freq / Fs);  // 2*PI*(freq/Fs), double (PI is a double literal)
   float arg = 0.0f;
-  // one step of the recurrence (src/filter.cpp:188-219)
-  auto pll_step = [&](float v) __attribute__((always_inline)) {
-    const float eI = (v == 0.0f ? 1.0f : v) * fbI;
-    const float eQ = v * (-1.0f * fbQ);
-    const float eD = (float)atan2((double)eQ, (double)eI);
-    integrator = integrator + Ki * eD;
-    phaseEst = phaseEst + (Kp * eD + integrator);
-    trigOffset = trigOffset + 1.0f;
-    arg = (float)(step * (double)trigOffset + (double)phaseEst);
-    double sv, cv;
-    sincos((double)arg, &sv, &cv);  // one argument reduction for both (same values as sin() and cos())
-    fbI = (float)cv;
-    fbQ = (float)sv;
+  // m exact steps of the recurrence from the current state (out of line)
+  auto exact_steps = [&](const float* buf, int m, long long k0) __attribute__((always_inline)) {
+    PllChunk c;
+#pragma unroll
+    for (int j = 0; j < kPllChunk; ++j) c.v[j] = j < m ? buf[j] : 0.0f;
+    const PllState p = pll_exact_chunk(PllState{fbI, fbQ, integrator, phaseEst, trigOffset, arg}, c, m, Kp, Ki, step,
+                                       ar, k0, n);
+    fbI = p.fbI;
+    fbQ = p.fbQ;
+    integrator = p.integrator;
+    phaseEst = p.phaseEst;
+    trigOffset = p.trigOffset;
+    arg = p.arg;
   };
   // the same step through pll_fast.hpp; score keeps the chunk's certificate
   struct DevOps {
@@ -159,11 +199,7 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
       phaseEst = s3;
       trigOffset = s4;
     }
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      pll_step(buf[j]);
-      if (k0 + j + 1 < n) ar[k0 + j + 1] = arg;
-    }
+    exact_steps(buf, CH, k0);
     if constexpr (FAST) {
       start_ok = gains_ok && pllfast::chunk_ok(fbI, fbQ, integrator, phaseEst, trigOffset, stepf);
       // the next chunk's first step rotates from the oscillator of this
@@ -188,16 +224,18 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
       run(xa, ga, k0 + CH, std::false_type{});
     }
   }
-  for (long long k = nc; k < n; ++k) {  // ragged tail
-    pll_step(x[k]);
-    if (k + 1 < n) ar[k + 1] = arg;
+  if (nc < n) {  // ragged tail
+    float tail[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) tail[j] = nc + j < n ? x[nc + j] : 0.0f;
+    exact_steps(tail, (int)(n - nc), nc);
   }
   st[0] = fbI;
   st[1] = fbQ;
   st[2] = integrator;
   st[3] = phaseEst;
   st[4] = trigOffset;
-  st[5] = (float)cos((double)(arg * nco_scale + phase_adjust));  // nco_state (:221-222)
+  st[5] = libmx::cos_f(arg * nco_scale + phase_adjust);  // nco_state (:221-222)
 }
 
 // guard[s * nchunk + c] = 1 when every sample of the PLL's chunk c of stream
@@ -225,7 +263,7 @@ __global__ __launch_bounds__(kWG) void nco_kernel(const float* __restrict__ args
   const long long k = (long long)blockIdx.x * kWG + threadIdx.x;
   if (k >= n) return;
   const float a = args[(long long)s * args_stride + k];
-  const float nco = k == 0 ? a : (float)cos((double)(a * nco_scale + phase_adjust));
+  const float nco = k == 0 ? a : libmx::cos_f(a * nco_scale + phase_adjust);
   out[(long long)s * out_stride + k] = mix ? nco * mix[(long long)s * mix_stride + k] * 2.0f : nco;
 }
 
@@ -258,7 +296,7 @@ hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, lon
   if (args_stride < n + 1) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((nstreams + 63) / 64)), block(64);
   const long long nchunk = n / kPllChunk;
-  // SDR_PLL_FAST=0 forces the library routines on every step (A/B, tests);
+  // SDR_PLL_FAST=0 runs libm_exact.hpp's routines on every step (A/B, tests);
   // SDR_PLL_GUARD=0 evaluates the input check inside the recurrence (A/B)
   const int fast = sw(kSwPllFast);  // (mode 2, no re-run path, exists in timing builds only)
   // (the pre-pass puts the streams on grid y: past the device's grid-y limit

@@ -115,6 +115,10 @@ _SIGS = {
     "sdr_stereo_back_dev": [_vp, C.c_float, _vp, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
+    "sdr_libm_sincos_hash_dev": [_vp, _i, C.c_uint, C.c_uint, _vp],
+    "sdr_libm_sincos_diff_dev": [_vp, C.c_uint, C.c_uint, _vp, _vp, _ll],
+    "sdr_libm_eval_dev": [_vp, _i, _vp, _vp, _ll, _vp],
+    "sdr_libm_atan2_screen_dev": [_vp, C.c_ulonglong, C.c_ulonglong, C.c_ulonglong, _vp, _ll, _vp, _ll, _vp],
 }
 _RESTYPE = {"sdr_version": C.c_char_p, "sdr_strerror": C.c_char_p, "sdr_ctx_last_error": C.c_char_p,
             "sdr_ctx_get_stream": _vp, "sdr_resample_out_len": _ll}
@@ -567,6 +571,23 @@ class Context:
 
     def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
         self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")
+
+    # -- the device transcendental routines of the PLL / NCO (libm_exact.hpp), in bulk
+    def libm_sincos_hash_dev(self, mode, chunk_lo, chunk_hi, hash_):
+        self._check(lib().sdr_libm_sincos_hash_dev(self._c, mode, chunk_lo, chunk_hi, _ptr(hash_)),
+                    "sdr_libm_sincos_hash_dev")
+
+    def libm_sincos_diff_dev(self, chunk_lo, chunk_hi, count, args, cap):
+        self._check(lib().sdr_libm_sincos_diff_dev(self._c, chunk_lo, chunk_hi, _ptr(count), _ptr(args), cap),
+                    "sdr_libm_sincos_diff_dev")
+
+    def libm_eval_dev(self, fn, a, b, n, out):
+        self._check(lib().sdr_libm_eval_dev(self._c, fn, _ptr(a), _ptr(b) if b is not None else None, n, _ptr(out)),
+                    "sdr_libm_eval_dev")
+
+    def libm_atan2_screen_dev(self, seed, first, count, cand, cand_cap, out, out_cap, counters):
+        self._check(lib().sdr_libm_atan2_screen_dev(self._c, seed, first, count, _ptr(cand), cand_cap, _ptr(out),
+                                                    out_cap, _ptr(counters)), "sdr_libm_atan2_screen_dev")
 
     def u8_to_planar_dev(self, iq, npairs, nstreams, iq_stride, I, Q, x_stride):
         self._check(lib().sdr_u8_to_planar_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, _ptr(I), _ptr(Q),

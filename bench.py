@@ -88,7 +88,16 @@ CONFIGS = {
     # bit-exact -- the line carries its error against the exact fp32 path
     "cfg5h": dict(kind="fir_block_f16", D=1, ntaps=1024, n=1048576, streams=2,
                   workload="fir1024_block1M_f16storage_IandQ"),
+    # config 5 as the kernel's streaming rate rather than one launch's fixed cost: 32
+    # independent 1 M-sample I/Q blocks (64 channel rows) per launch
+    "cfg5b": dict(kind="fir_block", D=1, ntaps=1024, n=1048576, streams=32, blocks=32,
+                  workload="fir1024_32blocks_of_1M_f32_IandQ"),
+    "cfg5hb": dict(kind="fir_block_f16", D=1, ntaps=1024, n=1048576, streams=32, blocks=32,
+                   workload="fir1024_32blocks_of_1M_f16storage_IandQ"),
 }
+# the fp16 arm's error sweep (cfg5h / cfg5hb lines): input amplitudes x tap counts
+F16_SWEEP_AMPS = [2.0 ** -k for k in range(8, -1, -1)]
+F16_SWEEP_TAPS = (64, 256, 1024, 4096)
 
 
 def parse(argv=None):
@@ -102,6 +111,7 @@ def parse(argv=None):
     ap.add_argument("--warm-seconds", type=float, default=0.25,
                     help="after the W warmup steps, keep running untimed steps for this long (clock ramp)")
     ap.add_argument("--no-fma-variant", action="store_true", help="skip the SDR_ARITH_FMA side measurement")
+    ap.add_argument("--no-f16-sweep", action="store_true", help="cfg5h/cfg5hb: skip the fp16 error sweep (setup)")
     ap.add_argument("--arith", choices=("exact", "fma"), default=os.environ.get("SDR_BENCH_ARITH", "exact"),
                     help="front-end FIR arithmetic: the reference's bits (exact) or one fused multiply-add per tap "
                          "(fma, tolerance-tested)")
@@ -176,7 +186,8 @@ CPU_KERNELS = {
     "cfg3": ("resample", 65600),
     # the 1024-tap block FIR on I and Q (src/filter.cpp:66-83); a 131,072-sample block keeps one
     # block of the sample within the time budget -- the rate per pair does not depend on it
-    "cfg5": ("fir1024", 131072), "cfg5h": ("fir1024", 131072),
+    "cfg5": ("fir1024", 131072), "cfg5h": ("fir1024", 131072), "cfg5b": ("fir1024", 131072),
+    "cfg5hb": ("fir1024", 131072),
     # the reference PROGRAM (src/project.cpp, mode 0), u8 IQ on stdin -> s16 PCM on stdout
     "mono0": ("program", "mono"), "stereo0": ("program", "stereo"), "stereo0w": ("program", "stereo"),
 }
@@ -457,59 +468,60 @@ class Job:
             self.metric = "IF MSamples/sec (input) through the polyphase resampler"
             # 55.5 FLOP per 4.7 B: above the exact-arithmetic ridge (78.65 TFLOP/s / 8 TB/s)
             self.bound = "valu"
-        elif kind == "fir_block":  # I and Q as two streams
-            out = torch.empty(S * n, dtype=torch.float32, device=dev)
-            IQs = [torch.stack([I[:n], Q[:n]]) for I, Q in planar]
-            self.keep += [out, IQs]
+        elif kind == "fir_block":  # I and Q of each block as two channel rows
+            nblk = cfg.get("blocks", 1)
+            nch = 2 * nblk
+            out = torch.empty(nch * n, dtype=torch.float32, device=dev)
+            stf = torch.zeros(nch * ns, dtype=torch.float32, device=dev)
+            IQs = [self._rows(I, Q, nblk, n) for I, Q in planar]
+            self.keep += [out, stf, IQs]
             for IQ in IQs:
-                steps.append(lambda IQ=IQ: ctx.fir_block_dev(IQ, n, 2, n, d_h, T, st0, ns, out, n))
-            self.units = n  # IQ pairs per step (I and Q each n samples)
+                steps.append(lambda IQ=IQ: ctx.fir_block_dev(IQ, n, nch, n, d_h, T, stf, ns, out, n))
+            self.units = nblk * n  # IQ pairs per step (I and Q each n samples per block)
             self.bytes_per_pair = 16.0
             self.flops_per_unit = 2.0 * 2 * T
             self.metric = "IQ MSamples/sec through a 1024-tap FIR"
             self.bound = "valu"
         else:  # fir_block_f16: fp16 storage of I and Q (converted once, untimed)
+            nblk = cfg.get("blocks", 1)
+            nch = 2 * nblk
             IQhs = []
             for I, Q in planar:
-                IQ = torch.stack([I[:n], Q[:n]])
-                IQh = torch.empty(2 * n, dtype=torch.float16, device=dev)
-                ctx.f32_to_f16_dev(IQ, 2 * n, IQh)
+                IQ = self._rows(I, Q, nblk, n)
+                IQh = torch.empty(nch * n, dtype=torch.float16, device=dev)
+                ctx.f32_to_f16_dev(IQ, nch * n, IQh)
                 IQhs.append(IQh)
-            sth = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
-            out = torch.empty(2 * n, dtype=torch.float32, device=dev)
+            sth = torch.zeros(nch * ns, dtype=torch.float16, device=dev)
+            out = torch.empty(nch * n, dtype=torch.float32, device=dev)
             # a tap plan: the MFMA kernel's fp16 tap copies built once (sdr_fir_f16_plan_create), as a
             # streaming caller with fixed taps would; bitwise the per-call path's outputs (tests)
             fplan = ctx.fir_f16_plan(d_h, T)
             self.keep += [IQhs, sth, out, fplan]
             if os.environ.get("SDR_BENCH_F16_PLAN", "1") != "0":
                 for IQh in IQhs:
-                    steps.append(lambda IQh=IQh: fplan.fir_block_f16_dev(IQh, n, 2, n, sth, ns, out, n))
+                    steps.append(lambda IQh=IQh: fplan.fir_block_f16_dev(IQh, n, nch, n, sth, ns, out, n))
             else:  # A/B: the tap copies built in every workgroup of every call
                 for IQh in IQhs:
-                    steps.append(lambda IQh=IQh: ctx.fir_block_f16_dev(IQh, n, 2, n, d_h, T, sth, ns, out, n))
-            self.units = n
+                    steps.append(lambda IQh=IQh: ctx.fir_block_f16_dev(IQh, n, nch, n, d_h, T, sth, ns, out, n))
+            self.units = nblk * n
             self.bytes_per_pair = 2.0 * 2 + 8.0  # fp16 in, fp32 out
             self.flops_per_unit = 2.0 * 2 * T
             self.metric = "IQ MSamples/sec through a 1024-tap FIR"
             self.bound = "valu"
-            # error of this arm against the exact fp32 path on the same first block
-            I, Q = planar[0]
-            IQ = torch.stack([I[:n], Q[:n]])
-            ref = torch.empty(2 * n, dtype=torch.float32, device=dev)
-            z32 = torch.zeros(2 * ns, dtype=torch.float32, device=dev)
-            ctx.fir_block_dev(IQ, n, 2, n, d_h, T, z32, ns, ref, n)
-            z16 = torch.zeros(2 * ns, dtype=torch.float16, device=dev)
-            got = torch.empty(2 * n, dtype=torch.float32, device=dev)
-            fplan.fir_block_f16_dev(IQhs[0], n, 2, n, z16, ns, got, n)
-            torch.cuda.synchronize(dev)
-            err = float((got - ref).abs().max())
-            scale = float(d_h.abs().sum()) * float(IQ.abs().max())
             self.f16_kernel = "mfma" if sdrhip.lib().sdr_fir_block_f16_kernel(T) else "dot2"
-            self.tolerance = {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale,
-                              "norm": "sum|h| * max|x|", "rms_err": float((got - ref).pow(2).mean().sqrt())}
+            # error of this arm against the exact fp32 path (src/filter.cpp:66-83) on the bench's own
+            # first block, and the sweep over input amplitudes x tap counts (untimed setup)
+            I, Q = planar[0]
+            self.tolerance = f16_error(ctx, torch, dev, sdrhip, torch.stack([I[:n], Q[:n]]), n, T)
+            if not args.no_f16_sweep:
+                self.tolerance["sweep"] = f16_sweep(ctx, torch, dev, sdrhip, torch.stack([I[:n], Q[:n]]), n)
         self.steps = steps
         self.graph = None
         torch.cuda.synchronize(dev)
+
+    def _rows(self, I, Q, nblk, n):
+        """[2 * nblk][n] channel rows: block b's I then Q (stream b of the synthetic batch)."""
+        return self.torch.stack([I.view(-1, n)[:nblk], Q.view(-1, n)[:nblk]], dim=1).reshape(2 * nblk, n).contiguous()
 
     # -- launching
     def launch(self, k: int):
@@ -599,6 +611,43 @@ class Job:
         if self.ctx2 is not None:
             self.ctx2.close()
         self.ctx.close()
+
+
+def f16_error(ctx, torch, dev, sdrhip, IQ, n, T, taps=None):
+    """The fp16 arm (fp16 storage, fp32 accumulation) against the exact fp32
+    blockConvolveFIR (src/filter.cpp:66-83) on the same two channel rows
+    [2][n], zero state: max / rms absolute error and the max normalised by
+    sum|h| * max|x|."""
+    h = torch.from_numpy(taps if taps is not None else sdrhip.taps_lpf(2.4e6, 100e3, T, 1)).to(dev)
+    ns = T - 1
+    ref = torch.empty(2 * n, dtype=torch.float32, device=dev)
+    ctx.fir_block_dev(IQ, n, 2, n, h, T, torch.zeros(2 * ns, dtype=torch.float32, device=dev), ns, ref, n)
+    IQh = torch.empty(2 * n, dtype=torch.float16, device=dev)
+    ctx.f32_to_f16_dev(IQ, 2 * n, IQh)
+    got = torch.empty(2 * n, dtype=torch.float32, device=dev)
+    ctx.fir_block_f16_dev(IQh, n, 2, n, h, T, torch.zeros(2 * ns, dtype=torch.float16, device=dev), ns, got, n)
+    torch.cuda.synchronize(dev)
+    d = (got.double() - ref.double()).abs()
+    err = float(d.max())
+    scale = float(h.abs().sum()) * float(IQ.abs().max())
+    return {"max_abs_err_vs_fp32_exact": err, "normalized": err / scale, "norm": "sum|h| * max|x|",
+            "rms_err": float(d.pow(2).mean().sqrt()), "rms_ref": float(ref.double().pow(2).mean().sqrt())}
+
+
+def f16_sweep(ctx, torch, dev, sdrhip, IQ, n):
+    """BASELINE config 5's fp32-vs-fp16 tolerance sweep: the fp16 arm's error
+    against the exact fp32 path for the synthetic I/Q scaled to each amplitude
+    in F16_SWEEP_AMPS, through impulseResponseLPF(2.4e6, 100e3, T) for each T
+    in F16_SWEEP_TAPS (untimed)."""
+    rows = []
+    for T in F16_SWEEP_TAPS:
+        taps = sdrhip.taps_lpf(2.4e6, 100e3, T, 1)
+        for a in F16_SWEEP_AMPS:
+            e = f16_error(ctx, torch, dev, sdrhip, (IQ * a).contiguous(), n, T, taps)
+            rows.append({"taps": T, "amplitude": a, "max_abs": e["max_abs_err_vs_fp32_exact"],
+                         "rms": e["rms_err"], "normalized": e["normalized"],
+                         "rms_rel": e["rms_err"] / e["rms_ref"] if e["rms_ref"] else None})
+    return rows
 
 
 def run_device(cfg_name, device, seed, args, barrier=None, side=True):

@@ -366,6 +366,36 @@ int sdr_synth_fm_u8_dev(sdr_ctx *ctx, uint8_t *iq, long long npairs, int nstream
 int sdr_u8_to_planar_dev(sdr_ctx *ctx, const uint8_t *iq, long long npairs, int nstreams, long long iq_stride,
                          float *I, float *Q, long long x_stride);
 
+/* ------------------------------------- device transcendental routines -- */
+/* The PLL and NCO kernels evaluate fmPLL's atan2 / sin / cos
+ * (src/filter.cpp:199-221: glibc's double routines on float arguments, each
+ * result stored to float) with csrc/libm_exact.hpp, built to give glibc's
+ * float for every argument.  These calls run those same device routines in
+ * bulk so the parity tests can prove it on the GPU (tests/test_libm_exact.py):
+ *   sdr_libm_sincos_hash_dev: every finite fp32 bit pattern u with u >> 20 in
+ *     [chunk_lo, chunk_hi) (2^20 per chunk; 4096 chunks cover all 2^32);
+ *     hash[chunk] += sum of a 64-bit mix of (u, sin float, cos float) -- zero
+ *     hash[] first.  mode 0: the product routine; 1: the platform library's
+ *     double sin / cos rounded to float (for comparison only).
+ *   sdr_libm_sincos_diff_dev: the arguments where the two differ:
+ *     args[2k] = u, args[2k+1] = 1 (sin) | 2 (cos), k < cap; *count (device,
+ *     zero it first) counts them all.
+ *   sdr_libm_eval_dev: out[i] = f(a[i] [, b[i]]) with fn 0 sin, 1 cos,
+ *     2 atan2(a, b) (product routines), 3 / 4 / 5 the platform library's.
+ *   sdr_libm_atan2_screen_dev: pairs first .. first+count-1 of a seeded
+ *     family; counters[0] (device, zeroed) counts those the short path does
+ *     not certify (offsets into cand, cap cand_cap), counters[1] those whose
+ *     exact value lies within 4 double ulps of a float rounding midpoint,
+ *     written to out[4k..4k+3] = {y, x, atan2 float, 0} bits (k < out_cap). */
+int sdr_libm_sincos_hash_dev(sdr_ctx *ctx, int mode, unsigned chunk_lo, unsigned chunk_hi,
+                             unsigned long long *hash);
+int sdr_libm_sincos_diff_dev(sdr_ctx *ctx, unsigned chunk_lo, unsigned chunk_hi, unsigned long long *count,
+                             unsigned *args, long long cap);
+int sdr_libm_eval_dev(sdr_ctx *ctx, int fn, const float *a, const float *b, long long n, float *out);
+int sdr_libm_atan2_screen_dev(sdr_ctx *ctx, unsigned long long seed, unsigned long long first,
+                              unsigned long long count, unsigned *cand, long long cand_cap, unsigned *out,
+                              long long out_cap, unsigned long long *counters);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,6 +2,7 @@
 # cfg3 ablations of the default resampler kernel (timing only; outputs wrong)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+. scripts/timing_lib.sh  # SDR_ABLATE etc. need the timing build
 OUT=gpurun_out/${TAG:-abl}
 mkdir -p "$OUT"
 for ab in ${ABL:-0 1 2}; do

@@ -5,6 +5,7 @@
 # region.   TAG=clk bash scripts/clock_probe.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+. scripts/timing_lib.sh  # SDR_ABLATE etc. need the timing build
 OUT=gpurun_out/${TAG:-clk}
 mkdir -p "$OUT"
 STEPS=${STEPS:-60000}

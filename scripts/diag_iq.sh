@@ -3,6 +3,7 @@
 # SQ counters of each, same box.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+. scripts/timing_lib.sh  # SDR_ABLATE etc. need the timing build
 OUT=gpurun_out/${TAG:-diag_iq}
 mkdir -p "$OUT"
 for v in 1 0; do

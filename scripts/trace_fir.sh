@@ -3,6 +3,7 @@
 # launch shapes: TAG=... bash scripts/trace_fir.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+. scripts/timing_lib.sh  # SDR_ABLATE etc. need the timing build
 OUT=gpurun_out/${TAG:-trace}
 mkdir -p "$OUT"
 export SDRHIP_LIB=$PWD/ab/trace.so SDR_FIR_IQ=0

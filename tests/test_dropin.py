@@ -203,16 +203,27 @@ def test_oracle_mono_chain_equals_reference_program(oracle, mode):
     assert np.array_equal(got, want)
 
 
+_MONO_CASES = [(m, p, 50) for m in (0, 1, 2, 3) for p in (0, 3)] + [(0, 0, 0), (0, 0, 256), (1, 0, 256), (0, 3, 0)]
+
+
+def _mono_state(nsd):
+    z = lambda k: np.zeros(k, np.float32)  # noqa: E731
+    return dict(i=z(100), q=z(100), prev=z(2), delay=z(nsd), audio=z(100))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("pad", [0, 3])
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
-def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode, pad):
+@pytest.mark.parametrize("mode,pad,nsd", _MONO_CASES)
+def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode, pad, nsd):
     """sdr_mono_pcm_u8_dev: several independent streams x 3 blocks, u8 IQ in,
     s16 PCM out, every byte equal to the oracle chain (itself pinned to the
-    reference program above); all carried state equal too.  pad = 0: wire
-    rows 8-B aligned -- at up == 1 the fused layout (delay line in the front
-    end's output row, PCM from the audio FIR); pad = 3: misaligned rows, the
-    generic front end and the separate delay / FIR / PCM launches."""
+    reference program above), and after every block every carried state --
+    RF FIR states, prev_I/Q, the delay line, the audio resampler state -- bit
+    for bit.  pad = 0: wire rows 8-B aligned -- at up == 1 the fused layout
+    (delay line in the front end's output row, carried through the kernels'
+    side copies; PCM from the audio FIR); pad = 3: misaligned rows, the
+    generic front end and the separate delay / FIR / PCM launches.  nsd: the
+    delay line's length (the reference's num_taps/2 = 50, src/project.cpp:114;
+    0 and 256 bound the fused layout's side copy)."""
     sdrhip = built_lib
     from sdrhip.synth import fm_iq_u8
 
@@ -221,27 +232,38 @@ def test_device_mono_pipeline(gpu_ctx, oracle, built_lib, mode, pad):
     npairs = block_bytes // 2
     na = sdrhip.resample_out_len(up, down, npairs // D)
     streams = [fm_iq_u8(npairs * nblk, seed=90 + 7 * s + mode, fs=rf_fs).tobytes() for s in range(nstreams)]
-    want = [_oracle_mono_stream(oracle, mode, streams[s], nblk) for s in range(nstreams)]
     A = sdrhip.DeviceArray
     d_hrf, d_ha = A.from_numpy(gpu_ctx, h_rf), A.from_numpy(gpu_ctx, h_audio)
-    z = lambda k: A.from_numpy(gpu_ctx, np.zeros(nstreams * k, np.float32))  # noqa: E731
-    si, sq, pi, pq, sd, sa = z(100), z(100), z(1), z(1), z(50), z(100)
+    z = lambda k: A.from_numpy(gpu_ctx, np.zeros(max(nstreams * k, 1), np.float32))  # noqa: E731
+    si, sq, pi, pq, sd, sa = z(100), z(100), z(1), z(1), z(nsd), z(100)
+    ost = [_mono_state(nsd) for _ in range(nstreams)]
     pcm_stride = na + 5
     d_pcm = A(gpu_ctx, nstreams * pcm_stride * 2)
-    got = [[] for _ in range(nstreams)]
     for b in range(nblk):
         blk = np.zeros((nstreams, block_bytes + pad), np.uint8)
         for s in range(nstreams):
             blk[s, :block_bytes] = np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
         d_iq = A.from_numpy(gpu_ctx, blk)
         gpu_ctx.mono_pcm_u8_dev(D, d_iq, npairs, nstreams, block_bytes + pad, d_hrf, len(h_rf), si, sq, 100, pi, pq,
-                                sd, 50, up, down, d_ha, len(h_audio), sa, 100, d_pcm, pcm_stride)
+                                sd, nsd, up, down, d_ha, len(h_audio), sa, 100, d_pcm, pcm_stride)
         gpu_ctx.synchronize()
         out = d_pcm.download(np.int16).reshape(nstreams, pcm_stride)[:, :na]
         for s in range(nstreams):
-            got[s].append(out[s].copy())
-    for s in range(nstreams):
-        assert np.array_equal(np.concatenate(got[s]), want[s]), f"stream {s}"
+            st = ost[s]
+            want = oracle.mono(D, blk[s, :block_bytes], h_rf, st["i"], st["q"], st["prev"], st["delay"], up, down,
+                               h_audio, st["audio"])
+            assert np.array_equal(out[s], want), f"stream {s} block {b}"
+        _assert_mono_state(si, sq, pi, pq, sd, sa, ost, nsd, f"block {b}")
+
+
+def _assert_mono_state(si, sq, pi, pq, sd, sa, ost, nsd, what):
+    n = len(ost)
+    for k, d, w in (("i", si, 100), ("q", sq, 100), ("audio", sa, 100)):
+        assert_bits(d.download().reshape(n, w), np.stack([o[k] for o in ost]), f"{k} state, {what}")
+    if nsd:
+        assert_bits(sd.download().reshape(n, nsd), np.stack([o["delay"] for o in ost]), f"delay state, {what}")
+    assert_bits(np.stack([pi.download(), pq.download()], axis=1), np.stack([o["prev"] for o in ost]),
+                f"prev_i/q, {what}")
 
 
 def _stereo_setup(oracle, mode):
@@ -397,6 +419,7 @@ def test_device_mono_random_blocks(gpu_ctx, oracle, built_lib, mode, npairs, nst
             want = oracle.mono(D, blk[s, :nb], h_rf, st["i"], st["q"], st["prev"], st["delay"], up, down, h_audio,
                                st["audio"])
             assert np.array_equal(out[s], want), f"stream {s} block {b}"
+        _assert_mono_state(si, sq, pi, pq, sd, sa, ost, 50, f"block {b}")
 
 
 _STEREO_RANDOM = []
