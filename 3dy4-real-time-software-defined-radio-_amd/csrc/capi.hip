@@ -244,7 +244,9 @@ int sw(Switch s) {
 
 extern "C" {
 
-const char* sdr_version(void) { return "sdrhip 0.1 (gfx950)"; }
+const char* sdr_version(void) { return "sdrhip 0.3 (gfx950, ABI 3)"; }
+
+int sdr_abi_version(void) { return SDR_ABI_VERSION; }
 
 const char* sdr_strerror(int code) {
   switch (code) {

@@ -46,6 +46,7 @@ _i = C.c_int
 # name -> argtypes (restype int unless listed in _RESTYPE)
 _SIGS = {
     "sdr_version": [],
+    "sdr_abi_version": [],
     "sdr_strerror": [_i],
     "sdr_device_count": [C.POINTER(_i)],
     "sdr_set_switch": [C.c_char_p, _i],
@@ -145,13 +146,20 @@ class SdrError(RuntimeError):
         super().__init__(f"{where}: {lib().sdr_strerror(code).decode()} ({detail})")
 
 
+ABI_VERSION = 3  # include/sdr_hip.h SDR_ABI_VERSION this binding was written for
+
+
 def lib() -> C.CDLL:
-    """Load libsdrhip.so (raises if it was not built -- no fallback)."""
+    """Load libsdrhip.so (raises if it was not built -- no fallback -- or if
+    its ABI version is not the one this binding was written for)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: build it (python -c 'import __graft_entry__ as g; g.build()')")
         L = C.CDLL(LIB_PATH)
+        L.sdr_abi_version.restype = _i
+        if L.sdr_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI {L.sdr_abi_version()}, this binding needs {ABI_VERSION}: rebuild")
         for name, args in _SIGS.items():
             f = getattr(L, name)
             f.argtypes = args

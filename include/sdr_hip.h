@@ -55,6 +55,17 @@ extern "C" {
 
 typedef struct sdr_ctx sdr_ctx;
 
+/* ABI version of this header; sdr_abi_version() returns the library's.  A
+ * caller built against version V should refuse a library whose version
+ * differs (entry points are added and, rarely, removed between versions --
+ * INTEGRATION.md §2 keeps the history).
+ *   1  rounds 1-4
+ *   2  round 5: the three-stage stereo split (sdr_stereo_pll_dev /
+ *      sdr_stereo_post_dev) removed; switch table (sdr_set_switch)
+ *   3  round 6: sdr_libm_* verification entry points added */
+#define SDR_ABI_VERSION 3
+int sdr_abi_version(void);
+
 /* ------------------------------------------------------------ context -- */
 const char *sdr_version(void);
 const char *sdr_strerror(int code);
