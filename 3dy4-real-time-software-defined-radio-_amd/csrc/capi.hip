@@ -1312,6 +1312,126 @@ int sdr_stereo_back_dev(sdr_ctx* c, float audio_fs, const sdr_stereo_taps* taps,
   return SDR_OK;
 }
 
+// ------------------------------------------------ mono path in two stages --
+// sdr_mono_pcm_u8_dev's work cut between the front end and the audio stage,
+// one block's demodulated row in a caller-owned work object, so block b+1's
+// front end can run on one context's stream while block b's audio stage runs
+// on another's (bench.py mono0, like the stereo pair above).  Disjoint state:
+// front = RF FIR states and prev_I/Q (src/project.cpp:86-90); back = the delay
+// line (:114) and the audio filter state (:116).  Unlike the one-call fused
+// layout (where the front end's tile-0 workgroups copy the delay line into the
+// row head), the back stage copies the delay line in itself -- the front end
+// of the next block may be running, and the delay line belongs to the back.
+struct sdr_mono_work {
+  int D = 0, up = 0, down = 0, nstreams = 0, ns_delay = 0;
+  long long npairs = 0, nd = 0, na = 0, rstride = 0, astride = 0;
+  bool fused = false;  // [delay head | demod] rows (up == 1, fast paths): the audio FIR reads them in place
+  void* mem = nullptr;
+  float *row = nullptr, *delayed = nullptr, *audio = nullptr;  // delayed / audio: the general layout only
+  StreamUses uses;
+};
+
+int sdr_mono_work_create(sdr_ctx* c, int D, long long npairs, int up, int down, int nstreams, int ns_delay,
+                         const float* h_rf, int rf_taps, int ns_rf, const float* h_audio, int audio_taps, int ns_audio,
+                         sdr_mono_work** out) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!out) return fail(c, SDR_EINVAL, "null work");
+  *out = nullptr;
+  if (D < 1 || npairs <= 0 || npairs % D || nstreams < 1 || up < 1 || down < 1 || ns_delay < 0)
+    return fail(c, SDR_EINVAL, "bad mono work shape");
+  auto* w = new sdr_mono_work;
+  w->D = D, w->up = up, w->down = down, w->nstreams = nstreams, w->npairs = npairs, w->ns_delay = ns_delay;
+  w->nd = npairs / D;
+  w->na = sdr_resample_out_len(up, down, w->nd);
+  if (w->na <= 0 || w->nd < ns_delay) {
+    delete w;
+    return fail(c, SDR_EINVAL, "empty audio block, or block shorter than the delay line");
+  }
+  // the fused layout's conditions (sdr_mono_pcm_u8_dev), row alignment aside
+  w->fused = up == 1 && h_rf && h_audio && ns_delay <= 256 && w->nd % down == 0 &&
+             sdr::fir_has_fast_path(D, rf_taps, ns_rf, 2, true, sdr::Src::U8) &&
+             sdr::fir_has_fast_path(down, audio_taps, ns_audio, 1, false, sdr::Src::F32);
+  w->rstride = ((w->fused ? ns_delay : 0) + w->nd + 3) / 4 * 4;
+  w->astride = (w->na + 3) / 4 * 4;
+  const size_t floats = (size_t)nstreams * (w->rstride + (w->fused ? 0 : w->rstride + w->astride));
+  if (hipMalloc(&w->mem, floats * sizeof(float)) != hipSuccess) {
+    delete w;
+    return fail(c, SDR_ENOMEM, "mono work buffers");
+  }
+  float* f = static_cast<float*>(w->mem);
+  w->row = f, f += (size_t)nstreams * w->rstride;
+  if (!w->fused) {
+    w->delayed = f, f += (size_t)nstreams * w->rstride;
+    w->audio = f;
+  }
+  *out = w;
+  return SDR_OK;
+}
+
+int sdr_mono_work_destroy(sdr_ctx* c, sdr_mono_work* w) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (w) {
+    w->uses.wait_and_release();  // the stages may have run on other contexts' streams
+    (void)hipFree(w->mem);
+    delete w;
+  }
+  return SDR_OK;
+}
+
+// src/project.cpp:72-93: the front end into the work's row
+int sdr_mono_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, const float* h_rf, int rf_taps,
+                          float* state_i, float* state_q, int ns_rf, float* prev_i, float* prev_q, sdr_mono_work* w) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!w) return fail(c, SDR_EINVAL, "null work");
+  rc = sdr_frontend_u8_dev(c, w->D, iq, w->npairs, w->nstreams, iq_stride, h_rf, rf_taps, state_i, state_q, ns_rf,
+                           prev_i, prev_q, w->row + (w->fused ? w->ns_delay : 0), w->rstride);
+  const hipError_t e = w->uses.mark(c->cur);  // marked even after a failed launch
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  return SDR_OK;
+}
+
+// src/project.cpp:114-118 + 304-314: delay line, audio filter, s16 PCM
+int sdr_mono_back_dev(sdr_ctx* c, const float* h_audio, int audio_taps, float* state_audio, int ns_audio,
+                      float* delay_state, sdr_mono_work* w, int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!w || !pcm || !delay_state) return fail(c, SDR_EINVAL, "null work / pcm / delay state");
+  const int n = w->nstreams;
+  if (n > 1 && pcm_stride < w->na) return fail(c, SDR_EINVAL, "pcm stride < audio samples per block");
+  if (w->fused) {
+    // the delay line into the row head (delayBlock's first ns_delay outputs,
+    // src/filter.cpp:230-238); the audio FIR then reads [head | demod] in
+    // place and copies the row's last ns_delay floats out as the new line
+    if (w->ns_delay > 0)
+      SDR_HIP(c, hipMemcpy2DAsync(w->row, (size_t)w->rstride * sizeof(float), delay_state,
+                                  (size_t)w->ns_delay * sizeof(float), (size_t)w->ns_delay * sizeof(float), (size_t)n,
+                                  hipMemcpyDeviceToDevice, c->cur));
+    sdr::FirLaunch tail;
+    std::memset(&tail, 0, sizeof tail);
+    tail.side_src = w->row + w->nd;
+    tail.side_src_stride = w->rstride;
+    tail.side_dst = delay_state;
+    tail.side_dst_stride = w->ns_delay;
+    tail.side_n = w->ns_delay;
+    rc = fir_decim_dev(c, w->down, w->row, w->nd, n, w->rstride, h_audio, audio_taps, state_audio, ns_audio, nullptr,
+                       0, &tail, pcm, n > 1 ? pcm_stride : w->na);
+  } else {
+    rc = sdr_delay_f32_dev(c, w->row, w->nd, n, w->rstride, delay_state, w->ns_delay, w->delayed, w->rstride);
+    if (!rc)
+      rc = sdr_resample_f32_dev(c, w->up, w->down, w->delayed, w->nd, n, w->rstride, h_audio, audio_taps, state_audio,
+                                ns_audio, w->audio, w->astride);
+    if (!rc) rc = sdr_pcm_s16_dev(c, w->audio, w->na, n, w->astride, pcm, pcm_stride);
+  }
+  const hipError_t e = w->uses.mark(c->cur);
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  return SDR_OK;
+}
+
 int sdr_synth_fm_u8_dev(sdr_ctx* c, uint8_t* iq, long long npairs, int nstreams, long long iq_stride,
                         unsigned long long seed) {
   int rc = enter(c);

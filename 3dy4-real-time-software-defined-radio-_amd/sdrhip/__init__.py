@@ -116,6 +116,10 @@ _SIGS = {
     "sdr_stereo_back_dev": [_vp, C.c_float, _vp, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
+    "sdr_mono_work_create": [_vp, _i, _ll, _i, _i, _i, _i, _vp, _i, _i, _vp, _i, _i, C.POINTER(_vp)],
+    "sdr_mono_work_destroy": [_vp, _vp],
+    "sdr_mono_front_u8_dev": [_vp, _vp, _ll, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp],
+    "sdr_mono_back_dev": [_vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _ll],
     "sdr_libm_sincos_hash_dev": [_vp, _i, C.c_uint, C.c_uint, _vp],
     "sdr_libm_sincos_diff_dev": [_vp, C.c_uint, C.c_uint, _vp, _vp, _ll],
     "sdr_libm_eval_dev": [_vp, _i, _vp, _vp, _ll, _vp],
@@ -343,6 +347,18 @@ class StereoWork:
     def close(self):
         if self._w and self._ctx._c:
             lib().sdr_stereo_work_destroy(self._ctx._c, self._w)
+        self._w = _vp()
+
+
+class MonoWork:
+    """sdr_mono_work: one block's demodulated row for mono_front/back."""
+
+    def __init__(self, ctx: "Context", w):
+        self._ctx, self._w = ctx, w
+
+    def close(self):
+        if self._w and self._ctx._c:
+            lib().sdr_mono_work_destroy(self._ctx._c, self._w)
         self._w = _vp()
 
 
@@ -576,6 +592,26 @@ class Context:
         """Back stage (PLL recurrence onwards, :123-132 + 304-314) from `work` to s16 L/R."""
         self._check(lib().sdr_stereo_back_dev(self._c, audio_fs, C.addressof(taps), C.addressof(state), work._w,
                                               _ptr(pcm), pcm_stride), "stereo_back_dev")
+
+    def mono_work(self, D, npairs, up, down, nstreams, ns_delay, h_rf, rf_taps, ns_rf, h_audio, audio_taps,
+                  ns_audio) -> "MonoWork":
+        """sdr_mono_work: one block's row for the two-stage mono calls (shape, taps and state lengths fixed)."""
+        w = _vp()
+        self._check(lib().sdr_mono_work_create(self._c, D, npairs, up, down, nstreams, ns_delay, _ptr(h_rf), rf_taps,
+                                               ns_rf, _ptr(h_audio), audio_taps, ns_audio, C.byref(w)),
+                    "mono_work_create")
+        return MonoWork(self, w)
+
+    def mono_front_u8_dev(self, iq, iq_stride, h_rf, rf_taps, state_i, state_q, ns_rf, prev_i, prev_q, work):
+        """Front stage of the mono path (src/project.cpp:72-93) into `work`."""
+        self._check(lib().sdr_mono_front_u8_dev(self._c, _ptr(iq), iq_stride, _ptr(h_rf), rf_taps, _ptr(state_i),
+                                                _ptr(state_q), ns_rf, _ptr(prev_i), _ptr(prev_q), work._w),
+                    "mono_front_u8_dev")
+
+    def mono_back_dev(self, h_audio, audio_taps, state_audio, ns_audio, delay_state, work, pcm, pcm_stride):
+        """Back stage (delay, audio filter, s16: :114-118 + 304-314) from `work`."""
+        self._check(lib().sdr_mono_back_dev(self._c, _ptr(h_audio), audio_taps, _ptr(state_audio), ns_audio,
+                                            _ptr(delay_state), work._w, _ptr(pcm), pcm_stride), "mono_back_dev")
 
     def synth_fm_u8_dev(self, iq, npairs, nstreams, iq_stride, seed=1234):
         self._check(lib().sdr_synth_fm_u8_dev(self._c, _ptr(iq), npairs, nstreams, iq_stride, seed), "synth")

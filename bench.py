@@ -125,6 +125,11 @@ def parse(argv=None):
                     help="stereo configs: 1 = each step as two stages on two contexts' streams (front end + band-pass "
                          "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence; 0 = "
                          "one call per step")
+    ap.add_argument("--mono-pipeline", type=int, choices=(0, 1),
+                    default=int(os.environ.get("SDR_BENCH_MONO_PIPE", "0")),
+                    help="mono0: 1 = each step as two stages on two contexts' streams (front end | delay + audio "
+                         "filter + PCM), step b+1's front end beside step b's audio stage; 0 = one call per step "
+                         "(the default: the pipelined form measured 2-7 %% slower, profiles/r06k/)")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
                     help="after the timed window, time this many seconds of back-to-back steps (the "
                          "`sustained` field: a receiver runs the block loop continuously); 0 skips it")
@@ -367,6 +372,35 @@ class Job:
             sa = torch.zeros(S * 100, dtype=torch.float32, device=dev)
             pcm = torch.empty(S * na, dtype=torch.int16, device=dev)
             self.keep += [sd, sa, pcm, d_ha]
+            if args.mono_pipeline:
+                # the step cut after the front end (sdr_mono_front_u8_dev | sdr_mono_back_dev,
+                # disjoint state): front stages on this context's stream, the audio stages on a
+                # second context's, two work objects in a ring -- block b+1's front end runs
+                # beside block b's audio filter (the stereo pair's scheme)
+                ctx2 = self.ctx2 = sdrhip.Context(device)
+                self.stream2 = torch.cuda.Stream(dev)
+                ctx2.set_stream(self.stream2.cuda_stream)
+                nslot = 2
+                works = [ctx.mono_work(D, n, up, down, S, 50, d_h, T, ns, d_ha, 101, 100) for _ in range(nslot)]
+                ev_f = [sdrhip.Event(ctx) for _ in range(nslot)]
+                ev_b = [sdrhip.Event(ctx) for _ in range(nslot)]
+                self.keep += [works, ev_f, ev_b]
+
+                def seq(j0, k):
+                    """k consecutive steps (see the stereo sequencer)."""
+                    for j in range(k):
+                        slot = (j0 + j) % nslot
+                        if j >= nslot:
+                            ev_b[slot].wait(ctx)
+                        ctx.mono_front_u8_dev(iqs[(j0 + j) % len(iqs)], 2 * n, d_h, T, st0, st1, ns, p0, p1,
+                                              works[slot])
+                        ev_f[slot].record(ctx)
+                        ev_f[slot].wait(ctx2)
+                        ctx2.mono_back_dev(d_ha, 101, sa, 100, sd, works[slot], pcm, na)
+                        ev_b[slot].record(ctx2)
+                    if k:
+                        ev_b[(j0 + k - 1) % nslot].wait(ctx)
+                self.seq = seq
             for iq in iqs:
                 steps.append(lambda iq=iq: ctx.mono_pcm_u8_dev(D, iq, n, S, 2 * n, d_h, T, st0, st1, ns, p0, p1, sd,
                                                                50, up, down, d_ha, 101, sa, 100, pcm, na))
@@ -844,6 +878,9 @@ def main(argv=None):
                        **({"stereo_pipeline": ("two stages on two contexts' streams (front | PLL onwards), step "
                                                "b+1's front overlapping step b's recurrence")
                            if args.stereo_pipeline else "one call per step"} if job["kind"] == "stereo_u8" else {}),
+                       **({"mono_pipeline": ("two stages on two contexts' streams (front end | delay + audio filter "
+                                             "+ PCM), step b+1's front end beside step b's audio stage")
+                           if args.mono_pipeline else "one call per step"} if job["kind"] == "mono_u8" else {}),
                        "state_carried_across_steps": True,
                        "arith": ("fma: one fused multiply-add per tap, tolerance-tested (DESIGN.md 2)"
                                  if args.arith == "fma" else "exact: the reference's bits")},

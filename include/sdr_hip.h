@@ -62,7 +62,8 @@ typedef struct sdr_ctx sdr_ctx;
  *   1  rounds 1-4
  *   2  round 5: the three-stage stereo split (sdr_stereo_pll_dev /
  *      sdr_stereo_post_dev) removed; switch table (sdr_set_switch)
- *   3  round 6: sdr_libm_* verification entry points added */
+ *   3  round 6: sdr_libm_* verification entry points, the two-stage mono
+ *      path (sdr_mono_work_*, sdr_mono_front_u8_dev, sdr_mono_back_dev) */
 #define SDR_ABI_VERSION 3
 int sdr_abi_version(void);
 
@@ -365,6 +366,28 @@ int sdr_stereo_front_u8_dev(sdr_ctx *ctx, const uint8_t *iq, long long iq_stride
                             sdr_stereo_state *state, sdr_stereo_work *work);
 int sdr_stereo_back_dev(sdr_ctx *ctx, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
                         sdr_stereo_work *work, int16_t *pcm, long long pcm_stride);
+
+/* The mono path in two stages (like the stereo pair above): sdr_mono_front_u8_dev
+ * runs the RF front end of one block into the work's row (src/project.cpp:72-93);
+ * sdr_mono_back_dev the delay line, the audio filter and the s16 stage
+ * (:114-118, 304-314).  The stages touch disjoint state (front: state_i/q,
+ * prev_i/q; back: delay_state, state_audio), so block b+1's front stage may run
+ * on one context's stream while block b's back stage runs on another's --
+ * order them with events and give each block in flight its own work.  The
+ * work is created for one shape and one set of tap / state lengths (it picks
+ * the fused row layout when up == 1 and the fast kernels cover the filters);
+ * outputs equal sdr_mono_pcm_u8_dev's.  destroy waits for every stream that
+ * used the work. */
+typedef struct sdr_mono_work sdr_mono_work;
+int sdr_mono_work_create(sdr_ctx *ctx, int D, long long npairs, int up, int down, int nstreams, int ns_delay,
+                         const float *h_rf, int rf_taps, int ns_rf, const float *h_audio, int audio_taps,
+                         int ns_audio, sdr_mono_work **work);
+int sdr_mono_work_destroy(sdr_ctx *ctx, sdr_mono_work *work);
+int sdr_mono_front_u8_dev(sdr_ctx *ctx, const uint8_t *iq, long long iq_stride, const float *h_rf, int rf_taps,
+                          float *state_i, float *state_q, int ns_rf, float *prev_i, float *prev_q,
+                          sdr_mono_work *work);
+int sdr_mono_back_dev(sdr_ctx *ctx, const float *h_audio, int audio_taps, float *state_audio, int ns_audio,
+                      float *delay_state, sdr_mono_work *work, int16_t *pcm, long long pcm_stride);
 
 /* ---------------------------------------------------- synthetic input -- */
 /* Fill nstreams x npairs interleaved u8 IQ of a noisy FM carrier on the

@@ -370,6 +370,70 @@ def test_device_stereo_pipeline(gpu_ctx, oracle, built_lib, mode, api):
 
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,nsd", [(0, 50), (1, 50), (2, 50), (3, 50), (0, 0), (1, 256)])
+def test_device_mono_two_stage(gpu_ctx, oracle, built_lib, mode, nsd):
+    """sdr_mono_front_u8_dev | sdr_mono_back_dev pipelined as bench.py's mono0
+    runs them: front stages on one context's stream, back stages on a second
+    context's, two work objects in a ring (front(b) waits for back(b-2), back(b)
+    for front(b)), everything enqueued before one synchronize -- so block b+1's
+    front end may run beside block b's audio stage.  3 streams x 5 blocks: PCM
+    bytes equal to the oracle chain for every block, and every carried state
+    after the last block.  Modes 0/1: the fused row layout; 2/3: the general
+    one (resampler)."""
+    sdrhip = built_lib
+    from sdrhip.synth import fm_iq_u8
+
+    rf_fs, D, up, down, block_bytes, h_rf, h_audio = _mono_setup(oracle, mode)
+    nstreams, nblk, nslot = 3, 5, 2
+    npairs = block_bytes // 2
+    na = sdrhip.resample_out_len(up, down, npairs // D)
+    streams = [fm_iq_u8(npairs * nblk, seed=310 + 7 * s + mode, fs=rf_fs).tobytes() for s in range(nstreams)]
+    A = sdrhip.DeviceArray
+    ctx2 = sdrhip.Context(0)
+    try:
+        d_hrf, d_ha = A.from_numpy(gpu_ctx, h_rf), A.from_numpy(gpu_ctx, h_audio)
+        z = lambda k: A.from_numpy(gpu_ctx, np.zeros(max(nstreams * k, 1), np.float32))  # noqa: E731
+        si, sq, pi, pq, sd, sa = z(100), z(100), z(1), z(1), z(nsd), z(100)
+        works = [gpu_ctx.mono_work(D, npairs, up, down, nstreams, nsd, d_hrf, len(h_rf), 100, d_ha, len(h_audio), 100)
+                 for _ in range(nslot)]
+        ev_f = [sdrhip.Event(gpu_ctx) for _ in range(nslot)]
+        ev_b = [sdrhip.Event(gpu_ctx) for _ in range(nslot)]
+        pcm_stride = na + 3
+        d_pcm = [A(gpu_ctx, nstreams * pcm_stride * 2) for _ in range(nblk)]
+        blks = []
+        for b in range(nblk):
+            blk = np.stack([np.frombuffer(streams[s][b * block_bytes:(b + 1) * block_bytes], np.uint8)
+                            for s in range(nstreams)])
+            blks.append(blk)
+        d_iq = [A.from_numpy(gpu_ctx, blk) for blk in blks]
+        gpu_ctx.synchronize()
+        for b in range(nblk):
+            slot = b % nslot
+            if b >= nslot:
+                ev_b[slot].wait(gpu_ctx)  # the slot's previous back stage has read its row
+            gpu_ctx.mono_front_u8_dev(d_iq[b], block_bytes, d_hrf, len(h_rf), si, sq, 100, pi, pq, works[slot])
+            ev_f[slot].record(gpu_ctx)
+            ev_f[slot].wait(ctx2)
+            ctx2.mono_back_dev(d_ha, len(h_audio), sa, 100, sd, works[slot], d_pcm[b], pcm_stride)
+            ev_b[slot].record(ctx2)
+        ctx2.synchronize()
+        gpu_ctx.synchronize()
+        ost = [_mono_state(nsd) for _ in range(nstreams)]
+        for b in range(nblk):
+            got = d_pcm[b].download(np.int16).reshape(nstreams, pcm_stride)[:, :na]
+            for s in range(nstreams):
+                st = ost[s]
+                want = oracle.mono(D, blks[b][s], h_rf, st["i"], st["q"], st["prev"], st["delay"], up, down, h_audio,
+                                   st["audio"])
+                assert np.array_equal(got[s], want), f"mode {mode} stream {s} block {b}"
+        _assert_mono_state(si, sq, pi, pq, sd, sa, ost, nsd, "after the last block")
+        for w in works:
+            w.close()
+    finally:
+        ctx2.close()
+
+
 _MRNG = np.random.default_rng(20261019)
 _MONO_RANDOM = []
 for _ in range(8):
