@@ -85,6 +85,14 @@ __global__ __launch_bounds__(256) void valu(float* out, int iters, float s) {
 #define A(V) { float t; asm volatile("v_mul_f32_dpp %1, %2, %3 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\tv_add_f32 %0, %1, %0" : "+v"(V.x), "=&v"(t) : "v"(c.y), "v"(V.y)); }
       REP8(A(a0) A(a1) A(a2) A(a3) A(a4) A(a5) A(a6) A(a7))
 #undef A
+    } else if constexpr (OP == 17) {  // v_fma_mix_f32 v, s, v(f16 lo), v(-0): an exact product from an f16 operand
+#define A(V) asm volatile("v_fma_mix_f32 %0, %2, %0, %3 op_sel_hi:[0,1,0]\n\tv_fma_mix_f32 %1, %2, %1, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "+v"(V.x), "+v"(V.y) : "s"(s), "v"(-0.0f));
+      REP8(A(a0) A(a1) A(a2) A(a3) A(a4) A(a5) A(a6) A(a7))
+#undef A
+    } else if constexpr (OP == 18) {  // fma_mix product (s, f16) + add, the add's chain dependent (the f16-staged FIR step)
+#define A(V) { float t; asm volatile("v_fma_mix_f32 %1, %2, %3, %4 op_sel_hi:[0,1,0]\n\tv_add_f32 %0, %1, %0" : "+v"(V.x), "=&v"(t) : "s"(s), "v"(V.y), "v"(-0.0f)); }
+      REP8(A(a0) A(a1) A(a2) A(a3) A(a4) A(a5) A(a6) A(a7))
+#undef A
     }
   }
   const f2 t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
@@ -105,9 +113,10 @@ int main() {
   const char* names[] = {"v_add_f32", "v_mul_f32 (s)", "v_fma_f32", "v_pk_add_f32", "v_pk_mul_f32 (s bcast)",
                          "v_pk_fma_f32", "pk_mul+pk_add", "mul+add",
                          "v_fma_f32 vvv", "v_mul_f32 vv", "v_fmac_f32 vv", "v_fmac_f32 sv", "v_add_f32 sv",
-                         "mul vv + add", "mul(s)+add (dep)", "v_mul_f32_dpp bcast", "mul_dpp+add (dep)"};
+                         "mul vv + add", "mul(s)+add (dep)", "v_mul_f32_dpp bcast", "mul_dpp+add (dep)",
+                         "v_fma_mix_f32 (s, f16, -0)", "fma_mix(s,f16)+add (dep)"};
   const int iters = 2000;
-  for (int op = 0; op < 17; ++op) {
+  for (int op = 0; op < 19; ++op) {
     for (int w : {1, 2, 3, 4, 8}) {  // waves per SIMD (256-thread WGs = 1 wave per SIMD each)
       const int grid = ncu * w;
       auto launch = [&] {
@@ -129,6 +138,8 @@ int main() {
           case 14: hipLaunchKernelGGL(valu<14>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
           case 15: hipLaunchKernelGGL(valu<15>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
           case 16: hipLaunchKernelGGL(valu<16>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
+          case 17: hipLaunchKernelGGL(valu<17>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
+          case 18: hipLaunchKernelGGL(valu<18>, dim3(grid), dim3(256), 0, 0, out, iters, 1.0001f); break;
         }
       };
       launch();
