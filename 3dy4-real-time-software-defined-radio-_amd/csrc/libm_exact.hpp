@@ -13,9 +13,11 @@
 // routines are built so that it can be shown:
 //   1. fast path: the short-chain kernels of pll_fast.hpp (relative error
 //      < 2^-46) with exact IEEE operations only (a true division instead of
-//      v_rcp_f64), certified by pll_fast's midpoint window (>= 1,024 double
-//      ulps from every float midpoint: the exact value and glibc's double, both
-//      within a few ulps, round to this float);
+//      v_rcp_f64), certified by pll_fast's midpoint windows (atan2: >= 1,024
+//      double ulps from every float midpoint: the exact value and glibc's
+//      double, both within a few ulps, round to this float; sin / cos: >= 32
+//      ulps, their kernels being within ~1.4 ulps -- the exhaustive sweep
+//      below checks every certified result);
 //   2. otherwise a double-double evaluation accurate to ~2^-70 relative
 //      (sin / cos: Payne-Hanek reduction of the fp32 argument against 320 bits
 //      of 2/pi, Taylor series in double-double; atan2: one Newton step on
@@ -302,7 +304,7 @@ SDR_HD inline __attribute__((always_inline)) SinCos sincos_f(float x) {
     pllfast::Osc o;
     float s, c;
     pllfast::sincos_fast<ExactOps>(x, s, c, score, o);
-    if (score >= pllfast::kCertified && normal_or_float(o.S) && normal_or_float(o.C)) return {s, c};
+    if (score >= pllfast::kCertifiedSc && normal_or_float(o.S) && normal_or_float(o.C)) return {s, c};
   } else {
     // beyond the fast reduction's checked range: Payne-Hanek, then the same
     // short kernels on the reduced argument's leading double
@@ -317,8 +319,8 @@ SDR_HD inline __attribute__((always_inline)) SinCos sincos_f(float x) {
     const double cr = __builtin_fma(z2, cp, __builtin_fma(z, -0.5, 1.0));
     dd S, C;
     quadrant(q, dd{sr, 0.0}, dd{cr, 0.0}, S, C);
-    const unsigned score = pllfast::umin(pllfast::mid_score(sr), pllfast::mid_score(cr));
-    if (score >= pllfast::kCertified && normal_or_float(sr) && normal_or_float(cr))
+    const unsigned score = pllfast::umin(pllfast::mid_score_sc(sr), pllfast::mid_score_sc(cr));
+    if (score >= pllfast::kCertifiedSc && normal_or_float(sr) && normal_or_float(cr))
       return {(float)(x < 0.0f ? -S.hi : S.hi), (float)C.hi};
   }
   return sincos_slow(x);

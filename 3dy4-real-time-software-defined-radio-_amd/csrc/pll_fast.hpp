@@ -94,6 +94,20 @@ constexpr unsigned kMidBias = 0u - (((1u << 28) - kCertW) << 3);  // -((2^28 - W
 SDR_HD inline unsigned lo_bits(double d) { return (unsigned)__builtin_bit_cast(unsigned long long, d); }
 SDR_HD inline unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
 SDR_HD inline unsigned mid_score(double d) { return (lo_bits(d) << 3) + kMidBias; }
+// The sine / cosine results keep their own, narrower window (round 6): their
+// kernels are accurate to ~2^-51.5 (about 1.4 double ulps, tests/pll_cert.cpp)
+// and, with a one-argument function, the window is PROVED rather than
+// sampled -- tests/libm_sweep.cpp runs sincos_fast on every finite float and
+// every result certified at kCertWSc ulps equals glibc's float.  Callers keep
+// a separate running minimum for it, compared against kCertifiedSc; a chunk
+// of the PLL then re-runs ~3x less often (the atan2 window stays 1,024 ulps).
+#ifndef SDR_PLL_CERT_W_SC
+#define SDR_PLL_CERT_W_SC 32
+#endif
+constexpr unsigned kCertWSc = SDR_PLL_CERT_W_SC;
+constexpr unsigned kCertifiedSc = (2u * kCertWSc) << 3;
+constexpr unsigned kMidBiasSc = 0u - (((1u << 28) - kCertWSc) << 3);
+SDR_HD inline unsigned mid_score_sc(double d) { return (lo_bits(d) << 3) + kMidBiasSc; }
 
 // The oscillator's argument over the next chunk's 8 steps stays inside the
 // reduction's exhaustively checked range, |trigArg| < 2^26:
@@ -202,7 +216,8 @@ struct Osc {
 };
 
 // (float)sin(x), (float)cos(x) for x an fp32 value in chunk_ok's domain
-// (|x| < 2^26, x != -0); folds both double results into score and leaves
+// (|x| < 2^26, x != -0); folds both double results into score -- the
+// sine / cosine running minimum, certified at >= kCertifiedSc -- and leaves
 // the oscillator in o.
 template <class Ops>
 SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score, Osc& o) {
@@ -221,7 +236,7 @@ SDR_HD inline void sincos_fast(float xf, float& sf, float& cf, unsigned& score, 
   // 1 - z/2 in one rounding (cos r >= 0.7: 1 ulp, no compensation needed)
   const double cp = Ops::fma(z2, Ops::fma(kC5, z2, Ops::fma(kC4, z, kC3)), Ops::fma(kC2, z, kC1));
   const double cr = Ops::fma(z2, cp, Ops::fma(z, -0.5, 1.0));
-  score = umin(score, umin(mid_score(sr), mid_score(cr)));
+  score = umin(score, umin(mid_score_sc(sr), mid_score_sc(cr)));
   // quadrant q mod 4: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s), applied
   // to the doubles (kept for atan2_rot) and then rounded (rounding commutes
   // with negation, so the floats are those of the rounded kernels)

@@ -121,12 +121,13 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     trigOffset = p.trigOffset;
     arg = p.arg;
   };
-  // the same step through pll_fast.hpp; score keeps the chunk's certificate
+  // the same step through pll_fast.hpp; score / score_sc keep the chunk's
+  // certificates (atan2 / sine and cosine: separate windows, pll_fast.hpp)
   struct DevOps {
     static __device__ double fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
     static __device__ double rcp(double u) { return __builtin_amdgcn_rcp(u); }
   };
-  unsigned score = 0u;
+  unsigned score = 0u, score_sc = 0u;
   // the oscillator the previous step left: every step but the kernel's first
   // rotates back from it (pllfast::atan2_rot) instead of evaluating atan2
   pllfast::Osc osc{0.0, 0.0, 1.0, 0};
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
     phaseEst = phaseEst + (Kp * eD + integrator);
     trigOffset = trigOffset + 1.0f;
     arg = (float)(step * (double)trigOffset + (double)phaseEst);
-    pllfast::sincos_fast<DevOps>(arg, fbQ, fbI, score, osc);
+    pllfast::sincos_fast<DevOps>(arg, fbQ, fbI, score_sc, osc);
   };
   using rot_t = std::true_type;
   using poly_t = std::false_type;
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
 #pragma unroll
         for (int j = 0; j < CH; ++j) in_ok &= (int)pllfast::input_ok(buf[j]);
       }
-      score = (start_ok && in_ok) ? ~0u : 0u;
+      score = score_sc = (start_ok && in_ok) ? ~0u : 0u;
       // unconditional: args rows hold n + 1 floats (launch_pll_recurrence), so
       // ar[n] is the row's spare slot -- no per-step bounds compare and branch
       if constexpr (decltype(first)::value)
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
       }
       start_ok = pllfast::chunk_end_ok(integrator, phaseEst, trigOffset, stepf);
       // 2: timing experiment only (no re-run)
-      if (FAST == 2 || !__any(score < pllfast::kCertified || !start_ok)) return;
+      if (FAST == 2 || !__any(score < pllfast::kCertified || score_sc < pllfast::kCertifiedSc || !start_ok)) return;
       fbI = s0;
       fbQ = s1;
       integrator = s2;

@@ -161,10 +161,18 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: build it (python -c 'import __graft_entry__ as g; g.build()')")
         L = C.CDLL(LIB_PATH)
-        L.sdr_abi_version.restype = _i
-        if L.sdr_abi_version() != ABI_VERSION:
-            raise ImportError(f"{LIB_PATH} has ABI {L.sdr_abi_version()}, this binding needs {ABI_VERSION}: rebuild")
+        # an explicitly named library (SDRHIP_LIB: a same-box A/B build of an
+        # older tree) may predate entry points; the shipped one may not
+        ab = bool(os.environ.get("SDRHIP_LIB"))
+        if hasattr(L, "sdr_abi_version"):
+            L.sdr_abi_version.restype = _i
+            if L.sdr_abi_version() != ABI_VERSION and not ab:
+                raise ImportError(f"{LIB_PATH} has ABI {L.sdr_abi_version()}, this binding needs {ABI_VERSION}: rebuild")
+        elif not ab:
+            raise ImportError(f"{LIB_PATH} has no sdr_abi_version (an older build): rebuild")
         for name, args in _SIGS.items():
+            if ab and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.argtypes = args
             f.restype = _RESTYPE.get(name, _i)

@@ -14,7 +14,9 @@ float arguments (src/filter.cpp:199-221).  This script runs tests/libm_sweep.cpp
                                  (argument bits, glibc sin float bits, glibc
                                  cos float bits, 1 = sin near | 2 = cos near);
                      meta        the sweep's JSON line (mismatches of
-                                 libm_exact against glibc: must be 0).
+                                 libm_exact against glibc, and of the PLL's
+                                 certified fast sine / cosine on |x| < 2^26:
+                                 must be 0).
   libm_atan2.npz   2^34 seeded pairs (tests/libm_sweep.cpp's four families):
                      near[m, 3]  every pair whose glibc double lies within 4
                                  ulps of a float midpoint: (y, x, glibc float);
@@ -48,32 +50,44 @@ def build(tmp: str) -> str:
     return exe
 
 
-def main(threads: int = os.cpu_count() or 8):
+def main(threads: int = os.cpu_count() or 8, only: str = ""):
     libc = platform.libc_ver()
     with tempfile.TemporaryDirectory() as tmp:
         exe = build(tmp)
-        pre = os.path.join(tmp, "sc")
-        line = subprocess.run([exe, "sincos", "0", "4096", str(threads), pre], check=True, capture_output=True,
-                              text=True).stdout.strip()
-        meta = json.loads(line)
-        assert meta["sin_mismatch"] == 0 and meta["cos_mismatch"] == 0 and meta["sincos_vs_sin_cos"] == 0, meta
-        meta["glibc"] = "-".join(libc)
-        h = np.fromfile(pre + ".hash", np.uint64)
-        near = np.fromfile(pre + ".near", np.uint32).reshape(-1, 4)
-        np.savez_compressed(os.path.join(HERE, "libm_sincos.npz"), hash=h, near=near,
-                            meta=np.array(json.dumps(meta)))
-        print("sincos", meta)
-        out = os.path.join(tmp, "at")
-        line = subprocess.run([exe, "atan2", str(ATAN2_SEED), str(ATAN2_LOG2), str(threads), out], check=True,
-                              capture_output=True, text=True).stdout.strip()
-        meta = json.loads(line)
-        assert meta["atan2_mismatch"] == 0, meta
-        meta.update(glibc="-".join(libc), seed=ATAN2_SEED, log2_pairs=ATAN2_LOG2)
-        near = np.fromfile(out, np.uint32).reshape(-1, 3)
-        near = near[np.lexsort((near[:, 1], near[:, 0]))]
-        np.savez_compressed(os.path.join(HERE, "libm_atan2.npz"), near=near, meta=np.array(json.dumps(meta)))
-        print("atan2", meta)
+        if only != "atan2":
+            sincos(exe, tmp, threads, libc)
+        if only != "sincos":
+            atan2(exe, tmp, threads, libc)
+
+
+def sincos(exe, tmp, threads, libc):
+    pre = os.path.join(tmp, "sc")
+    line = subprocess.run([exe, "sincos", "0", "4096", str(threads), pre], check=True, capture_output=True,
+                          text=True).stdout.strip()
+    meta = json.loads(line)
+    assert meta["sin_mismatch"] == 0 and meta["cos_mismatch"] == 0 and meta["sincos_vs_sin_cos"] == 0, meta
+    assert meta["fast_certified_mismatch"] == 0, meta
+    meta["glibc"] = "-".join(libc)
+    h = np.fromfile(pre + ".hash", np.uint64)
+    near = np.fromfile(pre + ".near", np.uint32).reshape(-1, 4)
+    np.savez_compressed(os.path.join(HERE, "libm_sincos.npz"), hash=h, near=near,
+                        meta=np.array(json.dumps(meta)))
+    print("sincos", meta)
+
+
+def atan2(exe, tmp, threads, libc):
+    out = os.path.join(tmp, "at")
+    line = subprocess.run([exe, "atan2", str(ATAN2_SEED), str(ATAN2_LOG2), str(threads), out], check=True,
+                          capture_output=True, text=True).stdout.strip()
+    meta = json.loads(line)
+    assert meta["atan2_mismatch"] == 0, meta
+    meta.update(glibc="-".join(libc), seed=ATAN2_SEED, log2_pairs=ATAN2_LOG2)
+    near = np.fromfile(out, np.uint32).reshape(-1, 3)
+    near = near[np.lexsort((near[:, 1], near[:, 0]))]
+    np.savez_compressed(os.path.join(HERE, "libm_atan2.npz"), near=near, meta=np.array(json.dumps(meta)))
+    print("atan2", meta)
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else (os.cpu_count() or 8))
+    # usage: make_libm_golden.py [threads] [sincos|atan2]  (both by default)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else (os.cpu_count() or 8), sys.argv[2] if len(sys.argv) > 2 else "")

@@ -67,13 +67,13 @@ static inline bool near_mid(double d) { return libmx::near_float_mid(d, 4.0); }
 
 static int sweep_sincos(int clo, int chi, int nth, const char* out) {
   std::atomic<int> next{clo};
-  std::atomic<long long> n{0}, bad_s{0}, bad_c{0}, bad_sc{0}, slow{0};
+  std::atomic<long long> n{0}, bad_s{0}, bad_c{0}, bad_sc{0}, slow{0}, fast_cert_bad{0};
   std::vector<uint64_t> hash(4096, 0);
   std::vector<uint32_t> near;
   std::mutex mu;
   auto work = [&] {
     std::vector<uint32_t> loc;
-    long long ln = 0, bs = 0, bc = 0, bsc = 0, sl = 0;
+    long long ln = 0, bs = 0, bc = 0, bsc = 0, sl = 0, fcm = 0;
     for (int ch; (ch = next.fetch_add(1)) < chi;) {
       uint64_t h = 0;
       for (uint32_t k = 0; k < (1u << 20); ++k) {
@@ -104,13 +104,19 @@ static int sweep_sincos(int clo, int chi, int nth, const char* out) {
           loc.push_back(fbits(gc));
           loc.push_back((ns ? 1u : 0u) | (nc ? 2u : 0u));
         }
-        // the double-double path's share (the fast path's certificate failed)
+        // the fast step the PLL kernel runs (pll_fast.hpp sincos_fast: fma
+        // only, the device's bits too) on its whole domain |x| < 2^26: every
+        // result its window certifies must be glibc's float -- the proof of
+        // kCertWSc -- and the rest is the double-double path's share
         if (std::fabs(x) < 0x1p26f && x != 0.0f) {
           unsigned score = ~0u;
           pllfast::Osc o;
           float a, b;
           pllfast::sincos_fast<libmx::ExactOps>(x, a, b, score, o);
-          sl += score < pllfast::kCertified;
+          if (score < pllfast::kCertifiedSc)
+            ++sl;
+          else if (fbits(a) != fbits(gs) || fbits(b) != fbits(gc))
+            ++fcm;
         }
       }
       hash[ch] = h;
@@ -122,14 +128,17 @@ static int sweep_sincos(int clo, int chi, int nth, const char* out) {
     bad_c += bc;
     bad_sc += bsc;
     slow += sl;
+    fast_cert_bad += fcm;
   };
   std::vector<std::thread> th;
   for (int t = 0; t < nth; ++t) th.emplace_back(work);
   for (auto& t : th) t.join();
   std::printf(
       "{\"args\": %lld, \"sin_mismatch\": %lld, \"cos_mismatch\": %lld, \"sincos_vs_sin_cos\": %lld, "
-      "\"near_midpoint\": %zu, \"fast_uncertified\": %lld}\n",
-      n.load(), bad_s.load(), bad_c.load(), bad_sc.load(), near.size() / 4, slow.load());
+      "\"near_midpoint\": %zu, \"fast_uncertified\": %lld, \"fast_certified_mismatch\": %lld, "
+      "\"cert_window_sc_ulps\": %u}\n",
+      n.load(), bad_s.load(), bad_c.load(), bad_sc.load(), near.size() / 4, slow.load(), fast_cert_bad.load(),
+      pllfast::kCertWSc);
   if (out) {
     // records sorted by argument bits (threads interleave chunks)
     std::vector<size_t> idx(near.size() / 4);

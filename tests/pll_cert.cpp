@@ -78,7 +78,7 @@ static void check_sincos(float x, Counts& c) {
   sincos_fast<HostOps>(x, s, co, score, o);
   const float rs = (float)std::sin((double)x), rc = (float)std::cos((double)x);
   ++c.n;
-  if (score < kCertified) return;
+  if (score < kCertifiedSc) return;
   ++c.certified;
   track(c, o.S, std::sin((double)x));
   track(c, o.C, std::cos((double)x));
@@ -152,7 +152,7 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
     const Pll saved = f;
     bool in_ok = true;
     for (long long j = 0; j < m; ++j) in_ok = in_ok && input_ok(in[k0 + j]);
-    unsigned score = start_ok && in_ok ? ~0u : 0u;
+    unsigned score = start_ok && in_ok ? ~0u : 0u, score_sc = score;
     for (long long j = 0; j < m; ++j) {
       const float v = in[k0 + j];
       const float eI = (v == 0.0f ? 1.0f : v) * f.fbI;
@@ -163,10 +163,10 @@ static long long pll_compare(const float* in, long long n, float trig0, long lon
       f.phase = f.phase + (Kp * eD + f.integ);
       f.trig = f.trig + 1.0f;
       fa[j] = (float)(step * (double)f.trig + (double)f.phase);
-      sincos_fast<HostOps>(fa[j], f.fbQ, f.fbI, score, osc);
+      sincos_fast<HostOps>(fa[j], f.fbQ, f.fbI, score_sc, osc);
     }
     start_ok = chunk_end_ok(f.integ, f.phase, f.trig, stepf);
-    const bool bad = score < kCertified || !start_ok;
+    const bool bad = score < kCertified || score_sc < kCertifiedSc || !start_ok;
     if (bad) {
       ++*reruns;
       f = saved;

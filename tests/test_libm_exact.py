@@ -78,6 +78,8 @@ def test_sincos_fixture_provenance():
     assert meta["args"] == 2 ** 32 - 2 ** 24, meta
     assert meta["sin_mismatch"] == 0 and meta["cos_mismatch"] == 0, meta
     assert meta["sincos_vs_sin_cos"] == 0, meta  # glibc's sincos == its sin and cos
+    # the PLL kernel's certified fast sine / cosine (pll_fast.hpp, window kCertWSc) on its whole domain
+    assert meta["fast_certified_mismatch"] == 0, meta
     assert g["hash"].shape == (4096,) and g["hash"].dtype == np.uint64
 
 
@@ -87,7 +89,7 @@ def test_sincos_slice(sweep, tmp_path, lo, hi):
     r = json.loads(subprocess.run([sweep, "sincos", str(lo), str(hi), "8", pre], check=True, capture_output=True,
                                   text=True).stdout)
     assert r["sin_mismatch"] == 0 and r["cos_mismatch"] == 0, r
-    assert r["sincos_vs_sin_cos"] == 0, r
+    assert r["sincos_vs_sin_cos"] == 0 and r["fast_certified_mismatch"] == 0, r
     h = np.fromfile(pre + ".hash", np.uint64)
     want = load_golden("libm_sincos")["hash"]
     assert np.array_equal(h[lo:hi], want[lo:hi]), "this host's glibc differs from the fixture's"
@@ -100,6 +102,7 @@ def test_sincos_every_float(sweep, tmp_path):
                                   capture_output=True, text=True).stdout)
     assert r["args"] == 2 ** 32 - 2 ** 24
     assert r["sin_mismatch"] == 0 and r["cos_mismatch"] == 0 and r["sincos_vs_sin_cos"] == 0, r
+    assert r["fast_certified_mismatch"] == 0, r
     assert np.array_equal(np.fromfile(pre + ".hash", np.uint64), load_golden("libm_sincos")["hash"])
 
 
