@@ -218,7 +218,8 @@ struct SwitchDef {
 constexpr SwitchDef kSwitchDefs[kSwCount] = {
     {"SDR_FIR_SC", 1},          {"SDR_FIR_SC_U8", 1},    {"SDR_RESAMPLE_LP", 1}, {"SDR_RESAMPLE_LOADER", 1},
     {"SDR_RESAMPLE_RS", 1},     {"SDR_RESAMPLE_PP", 1},  {"SDR_LONG_VTAP", 1},   {"SDR_F16_MFMA", 1},
-    {"SDR_F16_HEAD", 1},        {"SDR_F16_W8", 1},       {"SDR_PLL_FAST", 1},    {"SDR_PLL_GUARD", 1}};
+    {"SDR_F16_HEAD", 1},        {"SDR_F16_W8", 1},       {"SDR_PLL_FAST", 1},    {"SDR_PLL_GUARD", 1},
+    {"SDR_LONG_COMMIT", 1}};
 std::atomic<int> g_switch[kSwCount];
 std::once_flag g_switch_once;
 

@@ -41,6 +41,8 @@ struct LongArgs {
   int tiles_per_stream;
   int halo;   // roundup4(ntaps - 1)
   int img;    // LDS floats per workgroup image
+  float* commit;  // = state when only a stream's first workgroup reads the state (halo <= OUT_WG): it
+                  // writes the new state itself; nullptr: long_commit runs after the kernel
 };
 
 // VTAP = 1: the taps are staged in LDS behind the image and each pass's 32
@@ -145,6 +147,13 @@ __global__ __launch_bounds__(64 * kLongNW) void fir_long(LongArgs a) {
     for (int r = 0; r < R; ++r)
       if (m + r < a.n) ys[m + r] = acc[r];
   }
+  // state <- the last ns inputs (src/filter.cpp:82): this workgroup's image
+  // holds every old-state value any workgroup reads (staged before the
+  // barrier above), so the state is free to rewrite
+  if (a.commit != nullptr && tile == 0) {
+    float* nst = a.commit + (long long)s * a.ns;
+    for (int i = tid; i < a.ns; i += NTH) nst[i] = xs[a.n - a.ns + i];
+  }
 }
 
 // state <- last ns inputs, after every reader of the old state is done.
@@ -178,6 +187,10 @@ hipError_t launch_fir_long(const FirLaunch& f, const float* h, hipStream_t st) {
   a.tiles_per_stream = (int)((f.n + OUT_WG - 1) / OUT_WG);
   a.halo = (f.ntaps - 1 + 3) / 4 * 4;
   a.img = a.halo + OUT_WG + 4;
+  // tile 1 starts at OUT_WG - halo: with halo <= OUT_WG (T <= 1025) only tile 0
+  // reads the state, and it commits the new one in the same launch
+  const bool in_kernel = a.halo <= OUT_WG && sw(kSwLongCommit) != 0;
+  a.commit = in_kernel && f.ns > 0 ? f.state0 : nullptr;
   const long long blocks = (long long)a.tiles_per_stream * f.nstreams;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
   // LDS-staged taps (switch SDR_LONG_VTAP, measured at T = 1024) need 16-B
@@ -196,7 +209,7 @@ hipError_t launch_fir_long(const FirLaunch& f, const float* h, hipStream_t st) {
   else
     hipLaunchKernelGGL(fir_long<0>, dim3((unsigned)blocks), dim3(64 * kLongNW), lds_s, st, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || f.ns <= 0) return e;
+  if (e != hipSuccess || f.ns <= 0 || a.commit != nullptr) return e;
   hipLaunchKernelGGL(long_commit, dim3((f.ns + kWG - 1) / kWG, (unsigned)f.nstreams), dim3(kWG), 0, st, f.x0, f.n,
                      f.x_stride, f.state0, f.ns);
   return hipGetLastError();

@@ -104,6 +104,7 @@ enum Switch : int {
   kSwF16W8,           // SDR_F16_W8: fir_long_mfma as 8 waves of one tile (1) or 4 of two (0)
   kSwPllFast,         // SDR_PLL_FAST: certified short-chain PLL step (1) or library routines (0)
   kSwPllGuard,        // SDR_PLL_GUARD: the PLL's chunk input checks as a parallel pre-pass
+  kSwLongCommit,      // SDR_LONG_COMMIT: fir_long's first workgroup commits the state (1) or long_commit (0)
   kSwCount
 };
 int sw(Switch s);

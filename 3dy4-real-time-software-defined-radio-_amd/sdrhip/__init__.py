@@ -186,7 +186,7 @@ def version() -> str:
 
 SWITCHES = ("SDR_FIR_SC", "SDR_FIR_SC_U8", "SDR_RESAMPLE_LP", "SDR_RESAMPLE_LOADER", "SDR_RESAMPLE_RS",
             "SDR_RESAMPLE_PP", "SDR_LONG_VTAP", "SDR_F16_MFMA", "SDR_F16_HEAD", "SDR_F16_W8", "SDR_PLL_FAST",
-            "SDR_PLL_GUARD")
+            "SDR_PLL_GUARD", "SDR_LONG_COMMIT")
 
 
 def set_switch(name: str, value: int) -> None:

@@ -110,7 +110,7 @@ int sdr_ctx_set_stereo_fork(sdr_ctx *ctx, int mode);
  * sdr_set_switch: launches read it without scanning the environment.  Names:
  * SDR_FIR_SC, SDR_FIR_SC_U8, SDR_RESAMPLE_LP, SDR_RESAMPLE_LOADER,
  * SDR_RESAMPLE_RS, SDR_RESAMPLE_PP, SDR_LONG_VTAP, SDR_F16_MFMA,
- * SDR_F16_HEAD, SDR_F16_W8, SDR_PLL_FAST, SDR_PLL_GUARD.  An unknown name is
+ * SDR_F16_HEAD, SDR_F16_W8, SDR_PLL_FAST, SDR_PLL_GUARD, SDR_LONG_COMMIT.  An unknown name is
  * SDR_EINVAL.  A change applies to launches enqueued after it. */
 int sdr_set_switch(const char *name, int value);
 int sdr_get_switch(const char *name, int *value);

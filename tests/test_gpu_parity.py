@@ -850,6 +850,7 @@ def test_frontend_nonfinite_inputs(gpu_ctx, built_lib, kswitch, kernel):
 # kernel: which path runs the fixture (rows 16-B aligned or not, switches)
 NONFINITE_FIR = [("nonfinite_fir_101", "tileD1"), ("nonfinite_fir_101", "generic"),
                  ("nonfinite_fir_1024", "long"), ("nonfinite_fir_1024", "long_sgpr"),
+                 ("nonfinite_fir_1024", "long_commit0"),
                  ("nonfinite_fir_100", "generic"), ("nonfinite_decim_101", "grp"),
                  ("nonfinite_decim_101", "generic")]
 
@@ -868,6 +869,7 @@ def test_fir_block_nonfinite_inputs(gpu_ctx, built_lib, manifest, kswitch, name,
 
     sdrhip = built_lib
     kswitch("SDR_LONG_VTAP", 0 if kernel == "long_sgpr" else 1)
+    kswitch("SDR_LONG_COMMIT", 0 if kernel == "long_commit0" else 1)
     g = load_golden(name)
     p = manifest["cases"][name]["params"]
     S, D, block, ns, T = p["streams"], p["D"], p["block"], p["state"], p["ntaps"]
@@ -912,6 +914,35 @@ def test_demod_nonfinite_inputs(gpu_ctx, built_lib, manifest):
         pv = (g["prev0"] if i == 0 else g["prevs"][i - 1]).copy()
         assert_bits_nan(gpu_ctx.fm_demod(g["I"][a:b], g["Q"][a:b], pv), outs[-1], f"host call segment {i}")
     assert_bits_nan(np.concatenate(outs), g["out"], "demod")
+
+
+@pytest.mark.parametrize("commit", [1, 0])
+@pytest.mark.parametrize("ntaps,ns", [(64, 63), (1024, 1023), (1024, 1500), (1056, 1055)])
+def test_fir_long_state_commit(gpu_ctx, oracle, built_lib, kswitch, ntaps, ns, commit):
+    """blockConvolveFIR's state update (src/filter.cpp:82) under both commit
+    paths of fir_long: the stream's first workgroup writing the new state in
+    the filter's own launch (T <= 1,025: it is the old state's only reader),
+    or the separate long_commit launch (SDR_LONG_COMMIT=0, and always for
+    T = 1,056, whose second workgroup also reads the state) -- 3 streams x 3
+    blocks on padded rows, outputs and every state bitwise the oracle's."""
+    sdrhip = built_lib
+    kswitch("SDR_LONG_COMMIT", commit)
+    S, n, stride = 3, 5000, 5004
+    rng = np.random.default_rng(ntaps + ns)
+    h = (rng.standard_normal(ntaps) / ntaps).astype(np.float32)
+    st = rng.standard_normal((S, ns)).astype(np.float32)
+    ost = [st[s].copy() for s in range(S)]
+    A = sdrhip.DeviceArray
+    d_h, d_st, d_y = A.from_numpy(gpu_ctx, h), A.from_numpy(gpu_ctx, st), A(gpu_ctx, S * n * 4)
+    for b in range(3):
+        x = rng.standard_normal((S, n)).astype(np.float32)
+        d_x = A.from_numpy(gpu_ctx, _rows(x, stride))
+        gpu_ctx.fir_block_dev(d_x, n, S, stride, d_h, ntaps, d_st, ns, d_y, n)
+        gpu_ctx.synchronize()
+        got = d_y.download().reshape(S, n)
+        for s in range(S):
+            assert_bits(got[s], oracle.fir_block(x[s], h, ost[s]), f"stream {s} block {b}")
+        assert_bits(d_st.download().reshape(S, ns), np.stack(ost), f"state block {b}")
 
 
 def test_fir_long_8192_taps_both_tap_modes(gpu_ctx, oracle, built_lib, kswitch):
