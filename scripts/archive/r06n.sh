@@ -3,7 +3,7 @@
 # bench config with its CPU baseline (cfg5b / cfg5hb included).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-OUT=gpurun_out/r06n; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-r06n}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread \
   > $OUT/pytest_gpu.log 2>&1; rc=$?
 tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest_gpu.log | head; exit $rc; }
