@@ -512,3 +512,24 @@ def test_resample_plan_destroy_waits_for_other_context(built_lib, oracle):
             outs.append((d_y.download(), d_st.download()))
         assert_bits(outs[1][0], outs[0][0], "outputs with the plan destroyed mid-flight")
         assert_bits(outs[1][1], outs[0][1], "state with the plan destroyed mid-flight")
+
+
+def test_pll_fast_vs_library_screen(built_lib):
+    """fmPLL's certified short path (SDR_PLL_FAST=1) against its exact-library
+    path (libm_exact: glibc's floats) at stereo0w's stream count: 16,384
+    streams x 6 blocks of 5,120 pilot samples (5.0e8 PLL steps, state carried),
+    every NCO output and state float bitwise equal (tests/pll_screen.py; the
+    long screens it prints are in profiles/).  src/filter.cpp:174-228.  A
+    child process: the screen's torch must open the device before the
+    library does."""
+    import json
+    import os
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pll_screen.py")
+    p = subprocess.run([sys.executable, script, "--streams", "16384", "--blocks", "6", "--seed", "7"],
+                       capture_output=True, text=True, timeout=200)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["pll_steps"] == 16384 * 5120 * 6, r
+    assert r["output_mismatches"] == 0 and r["state_mismatches"] == 0, r
