@@ -748,8 +748,10 @@ def roofline(job: dict, ms_per_step: float, config: str, arith: str = "exact") -
         roof = {"bound": "hbm", "achieved": round(bw, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hbm_frac, 4)}
     else:
-        roof = {"bound": "valu", "achieved": round(fl, 2), "peak": round(vpeak, 2), "unit": "TFLOP/s",
-                "frac": round(valu_frac, 4)}
+        # the fp16 arm's compute roof is the matrix cores' (dense fp16 MFMA); every
+        # other compute-bound line is priced against the VALU issue of its arithmetic
+        roof = {"bound": "mfma" if f16_mfma else "valu", "achieved": round(fl, 2), "peak": round(vpeak, 2),
+                "unit": "TFLOP/s", "frac": round(valu_frac, 4)}
     roof["hbm_frac"] = round(hbm_frac, 4)
     roof["valu_frac"] = round(valu_frac, 4)
     roof["valu_peak_tflops"] = round(vpeak, 2)

@@ -193,6 +193,11 @@ def test_roofline_picks_the_binding_roof():
     r = b.roofline(cfg3, 0.136, "none")
     assert r["bound"] == "valu" and r["frac"] == r["valu_frac"]
     assert r["hbm_frac"] == pytest.approx(0.29, abs=0.01)
+    # the fp16 arm on the matrix cores: priced against the dense fp16 MFMA peak, bound "mfma"
+    cfg5h = dict(base, units=2 * 1048576, bytes_per_pair=6.0, flops_per_unit=2.0 * 1024, kind="fir_block_f16",
+                 f16_kernel="mfma")
+    r = b.roofline(cfg5h, 0.0062, "none")
+    assert r["bound"] == "mfma" and r["peak"] == pytest.approx(2500.0) and r["frac"] == r["valu_frac"]
 
 
 @pytest.mark.parametrize("config", ["cfg2", "cfg3", "cfg5h", "mono0", "stereo0"])
