@@ -917,17 +917,19 @@ def test_demod_nonfinite_inputs(gpu_ctx, built_lib, manifest):
 
 
 @pytest.mark.parametrize("commit", [1, 0])
-@pytest.mark.parametrize("ntaps,ns", [(64, 63), (1024, 1023), (1024, 1500), (1056, 1055)])
-def test_fir_long_state_commit(gpu_ctx, oracle, built_lib, kswitch, ntaps, ns, commit):
+@pytest.mark.parametrize("ntaps,ns,n", [(64, 63, 5000), (64, 63, 900), (1024, 1023, 5000), (1024, 1500, 5000),
+                                        (1056, 1055, 5000)])
+def test_fir_long_state_commit(gpu_ctx, oracle, built_lib, kswitch, ntaps, ns, n, commit):
     """blockConvolveFIR's state update (src/filter.cpp:82) under both commit
     paths of fir_long: the stream's first workgroup writing the new state in
     the filter's own launch (T <= 1,025: it is the old state's only reader),
     or the separate long_commit launch (SDR_LONG_COMMIT=0, and always for
     T = 1,056, whose second workgroup also reads the state) -- 3 streams x 3
-    blocks on padded rows, outputs and every state bitwise the oracle's."""
+    blocks on padded rows, outputs and every state bitwise the oracle's; n = 900
+    is one workgroup per stream (it reads and rewrites the state alone)."""
     sdrhip = built_lib
     kswitch("SDR_LONG_COMMIT", commit)
-    S, n, stride = 3, 5000, 5004
+    S, stride = 3, n + 4
     rng = np.random.default_rng(ntaps + ns)
     h = (rng.standard_normal(ntaps) / ntaps).astype(np.float32)
     st = rng.standard_normal((S, ns)).astype(np.float32)
