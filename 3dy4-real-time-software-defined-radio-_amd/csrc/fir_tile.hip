@@ -1364,15 +1364,14 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
     // tiles (edge_fill rewrites what a stored output reads of them).
     if (SDR_ABL(a.ablate) != 1) {
       const long long pmax = (n & ~3LL) - 4;
-#pragma unroll
-      for (int it = 0; it <= G::FULL; ++it) {
-        if (it == G::FULL && !(G::REM && lane < G::REM)) break;
-        long long p = tr.pb + 4LL * (lane + it * NTH);
+      auto dma = [&](int i, int row) __attribute__((always_inline)) {
+        long long p = tr.pb + 4LL * i;
         p = p < 0 ? 0 : (p > pmax ? pmax : p);
-#if defined(__HIP_DEVICE_COMPILE__)  // a device builtin: the host pass would drop the kernel's stub
-        __builtin_amdgcn_global_load_lds(tr.x0 + p, lds + 4 * G::NTH * it, 16, 0, SDR_FIR_NT ? 2 : 0);
-#endif
-      }
+        __builtin_amdgcn_global_load_lds(tr.x0 + p, lds + 4 * G::NTH * row, 16, 0, SDR_FIR_NT ? 2 : 0);
+      };
+#pragma unroll
+      for (int it = 0; it < G::FULL; ++it) dma(lane + it * NTH, it);
+      if (G::REM && lane < G::REM) dma(lane + G::FULL * NTH, G::FULL);
     }
   } else if (SDR_ABL(a.ablate) != 1) {
     stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
