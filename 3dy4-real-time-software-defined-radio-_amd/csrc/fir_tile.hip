@@ -82,12 +82,6 @@
 // SDR_SC_T0PRE: fir_tile_sc's tile 0 issues its extra loads (carried state,
 // block tail, side copy) with the span's (one memory latency, not three);
 // f32 front end: cfg2 0.0954-0.0959 vs 0.0959-0.0963 ms (profiles/r05u/)
-// SDR_SC_DMA: fir_tile_sc's f32 span staged by LDS-DMA (global_load_lds,
-// 16 B per lane straight into the wave's slice) instead of loads into
-// registers and ds_write_b128 (A/B)
-#ifndef SDR_SC_DMA
-#define SDR_SC_DMA 0
-#endif
 #ifndef SDR_SC_T0PRE
 #define SDR_SC_T0PRE 1
 #endif
@@ -1357,25 +1351,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
   Stage v;
 #pragma unroll
   for (int i = 0; i <= G::FULL; ++i) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr bool kDma = SDR_SC_DMA && SRC == Src::F32;
-  if constexpr (kDma) {
-    // chunk i of the span -> lds[4 i .. 4 i + 3]: lane l of row `it` lands at
-    // the row's wave-uniform base + 16 l.  Clamped like stage_load's edge
-    // tiles (edge_fill rewrites what a stored output reads of them).
-    if (SDR_ABL(a.ablate) != 1) {
-      const long long pmax = (n & ~3LL) - 4;
-      auto dma = [&](int i, int row) __attribute__((always_inline)) {
-        long long p = tr.pb + 4LL * i;
-        p = p < 0 ? 0 : (p > pmax ? pmax : p);
-        __builtin_amdgcn_global_load_lds(tr.x0 + p, lds + 4 * G::NTH * row, 16, 0, SDR_FIR_NT ? 2 : 0);
-      };
-#pragma unroll
-      for (int it = 0; it < G::FULL; ++it) dma(lane + it * NTH, it);
-      if (G::REM && lane < G::REM) dma(lane + G::FULL * NTH, G::FULL);
-    }
-  } else if (SDR_ABL(a.ablate) != 1) {
-    stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
-  }
+  if (SDR_ABL(a.ablate) != 1) stage_load<D, T, R, DEMOD, NW, 1, SRC>(tr, n, lane, v, v);
   // Tile 0's own inputs go out in the span's load batch (SDR_SC_T0PRE): the
   // carried state under the span's head, the block's last STRIP inputs (the
   // prev_* recompute and the new state) and the side copy -- one memory
@@ -1409,10 +1385,7 @@ __global__ __launch_bounds__(128) void fir_tile_sc(FirLaunch a, const float* __r
 #pragma unroll
     for (int u = 0; u < kTp; ++u) h_pre[u] = h[min(lane + 64 * u, T - 1)];
   }
-  if constexpr (kDma) {
-    // the span has landed in LDS before anything below rewrites part of it
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if constexpr (SRC == Src::F32) {
+  if constexpr (SRC == Src::F32) {
     stage_store<D, T, R, DEMOD, NW, 1, SRC>(lds, lds, lane, v, v);
   } else {
     // u8 wire format: both waves load the interleaved bytes (I0 Q0 I1 Q1 | I2 Q2 I3 Q3
