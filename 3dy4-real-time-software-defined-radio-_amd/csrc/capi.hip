@@ -1186,6 +1186,7 @@ struct sdr_stereo_work {
   float *demod = nullptr, *delayed = nullptr, *mono = nullptr, *pilot = nullptr, *sband = nullptr, *slp = nullptr,
         *args = nullptr, *mixed = nullptr;
   uint8_t* guard = nullptr;
+  bool guard_ready = false;  // the front stage wrote this block's PLL guard (host order: front, then back)
   StreamUses uses;  // every stream a stage ran on (destroy waits for them)
 };
 
@@ -1263,9 +1264,15 @@ int sdr_stereo_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, 
   if (!rc)
     rc = sdr_fir_block_f32_dev(c, w->demod, w->nd, n, w->dstride, taps->h_pilot, taps->bpf_taps, st->pilot_state,
                                st->ns_bpf, w->pilot, w->dstride);
+  // the recurrence's input guard from the pilot, here: off the back stage's
+  // critical path (the back stage waits for this stage anyway)
+  w->guard_ready = false;
+  hipError_t ge = hipSuccess;
+  if (!rc) ge = sdr::launch_pll_guard(w->pilot, w->nd, n, w->dstride, w->guard, c->cur, &w->guard_ready);
   // marked even after a failed launch: whatever was enqueued uses the work
   const hipError_t e = w->uses.mark(c->cur);
   if (rc) return rc;
+  if (ge != hipSuccess) return hip_fail(c, ge, "pll guard launch");
   if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   return SDR_OK;
 }
@@ -1276,7 +1283,8 @@ int sdr_stereo_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, 
 static int stereo_pll(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_stereo_work* w) {
   if (!st || !w) return fail(c, SDR_EINVAL, "null state / work");
   hipError_t e = sdr::launch_pll_recurrence(w->pilot, w->nd, w->nstreams, w->dstride, 19e3f, audio_fs, 2.0f, 0.0f,
-                                            0.01f, st->pll, w->args, w->pstride, c->cur, w->guard);
+                                            0.01f, st->pll, w->args, w->pstride, c->cur, w->guard, w->guard_ready);
+  w->guard_ready = false;  // one block's guard serves one recurrence
   if (e != hipSuccess) return hip_fail(c, e, "pll launch");
   return SDR_OK;
 }

@@ -148,9 +148,16 @@ hipError_t launch_pll(const float* in, long long n, int nstreams, long long in_s
                       hipStream_t st, uint8_t* guard);
 // the two halves of launch_pll: the per-stream recurrence (records each
 // sample's oscillator argument in args) and the parallel NCO (+ mixer)
+// guard_ready: launch_pll_guard already wrote this block's guard (stream-ordered
+// before this launch; the two-stage stereo front stage does, off the recurrence's
+// critical path), else the pre-pass runs here first
 hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
                                  float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
-                                 long long args_stride, hipStream_t st, uint8_t* guard);
+                                 long long args_stride, hipStream_t st, uint8_t* guard, bool guard_ready = false);
+// the recurrence's input guard pre-pass alone; *ready = whether it ran (the
+// recurrence then takes the guard as given)
+hipError_t launch_pll_guard(const float* in, long long n, int nstreams, long long in_stride, uint8_t* guard,
+                            hipStream_t st, bool* ready);
 hipError_t launch_nco(const float* args, long long args_stride, long long n, int nstreams, float nco_scale,
                       float phase_adjust, const float* mix, long long mix_stride, float* out, long long out_stride,
                       hipStream_t st);

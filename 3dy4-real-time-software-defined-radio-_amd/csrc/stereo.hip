@@ -241,7 +241,28 @@ __global__ __launch_bounds__(64) void pll_kernel(const float* __restrict__ in, l
 
 // guard[s * nchunk + c] = 1 when every sample of the PLL's chunk c of stream
 // s passes pllfast::input_ok (0 or 2^-60 <= |v| <= FLT_MAX): the chunk guard
-// of the certified step, for all streams and chunks at once.
+// of the certified step, for all streams and chunks at once.  It sits on the
+// stereo back stage's critical path, right before the recurrence, so it reads
+// like a streaming kernel: one 16-B load per lane (a chunk is lanes 2c and
+// 2c + 1, combined by a lane swap), the rows 16-B aligned
+// (pll_guard_vec_ok); pll_guard_kernel below takes any other row layout.
+static_assert(kPllChunk == 8, "a chunk is two float4 lanes");
+__global__ __launch_bounds__(kWG) void pll_guard_vec_kernel(const float* __restrict__ in, long long in_stride,
+                                                            uint8_t* __restrict__ guard, long long nchunk) {
+  const int s = blockIdx.y;
+  const long long q = (long long)blockIdx.x * kWG + threadIdx.x;  // the stream's q-th float4
+  int ok = 1;
+  if (q < 2 * nchunk) {
+    const float4 v = *reinterpret_cast<const float4*>(in + (long long)s * in_stride + 4 * q);
+    ok = (int)pllfast::input_ok(v.x) & (int)pllfast::input_ok(v.y) & (int)pllfast::input_ok(v.z) &
+         (int)pllfast::input_ok(v.w);
+  }
+  ok &= __shfl_xor(ok, 1, 64);
+  if (q < 2 * nchunk && (q & 1) == 0) guard[(long long)s * nchunk + (q >> 1)] = (uint8_t)ok;
+}
+bool pll_guard_vec_ok(const float* in, long long in_stride) {
+  return (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (in_stride & 3) == 0;
+}
 __global__ __launch_bounds__(kWG) void pll_guard_kernel(const float* __restrict__ in, int nstreams, long long in_stride,
                                                         uint8_t* __restrict__ guard, long long nchunk) {
   const int s = blockIdx.y;
@@ -291,22 +312,41 @@ size_t pll_guard_bytes(long long n, int nstreams) {
   return (size_t)(nchunk > 0 ? nchunk : 1) * (size_t)(nstreams > 0 ? nstreams : 1);
 }
 
+// The guard pre-pass runs when the certified step does and the streams fit
+// the grid's y dimension (past the device's grid-y limit the recurrence
+// evaluates the guard itself -- same bits); SDR_PLL_FAST=0 runs
+// libm_exact.hpp's routines on every step (A/B, tests), SDR_PLL_GUARD=0
+// evaluates the input check inside the recurrence (A/B).
+static bool pll_guard_pre(long long n, int nstreams) {
+  return n / kPllChunk > 0 && sw(kSwPllFast) != 0 && sw(kSwPllGuard) != 0 && nstreams <= device_grid_y_max();
+}
+
+hipError_t launch_pll_guard(const float* in, long long n, int nstreams, long long in_stride, uint8_t* guard,
+                            hipStream_t st, bool* ready) {
+  *ready = false;
+  if (!guard || !pll_guard_pre(n, nstreams)) return hipSuccess;
+  const long long nchunk = n / kPllChunk;
+  if (pll_guard_vec_ok(in, in_stride))
+    hipLaunchKernelGGL(pll_guard_vec_kernel, dim3((unsigned)((2 * nchunk + kWG - 1) / kWG), (unsigned)nstreams),
+                       dim3(kWG), 0, st, in, in_stride, guard, nchunk);
+  else
+    hipLaunchKernelGGL(pll_guard_kernel, dim3((unsigned)((nchunk + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0,
+                       st, in, nstreams, in_stride, guard, nchunk);
+  const hipError_t e = hipGetLastError();
+  *ready = e == hipSuccess;
+  return e;
+}
+
 hipError_t launch_pll_recurrence(const float* in, long long n, int nstreams, long long in_stride, float freq,
                                  float Fs, float nco_scale, float phase_adjust, float norm_bw, float* pll, float* args,
-                                 long long args_stride, hipStream_t st, uint8_t* guard) {
+                                 long long args_stride, hipStream_t st, uint8_t* guard, bool guard_ready) {
   if (args_stride < n + 1) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((nstreams + 63) / 64)), block(64);
   const long long nchunk = n / kPllChunk;
-  // SDR_PLL_FAST=0 runs libm_exact.hpp's routines on every step (A/B, tests);
-  // SDR_PLL_GUARD=0 evaluates the input check inside the recurrence (A/B)
   const int fast = sw(kSwPllFast);  // (mode 2, no re-run path, exists in timing builds only)
-  // (the pre-pass puts the streams on grid y: past the device's grid-y limit
-  // the recurrence evaluates the guard itself -- same bits)
-  const bool pre = guard && nchunk > 0 && sw(kSwPllGuard) != 0 && nstreams <= device_grid_y_max();
-  if (fast && pre) {
-    hipLaunchKernelGGL(pll_guard_kernel, dim3((unsigned)((nchunk + kWG - 1) / kWG), (unsigned)nstreams), dim3(kWG), 0,
-                       st, in, nstreams, in_stride, guard, nchunk);
-    const hipError_t e = hipGetLastError();
+  bool pre = guard_ready;
+  if (!pre) {
+    const hipError_t e = launch_pll_guard(in, n, nstreams, in_stride, guard, st, &pre);
     if (e != hipSuccess) return e;
   }
 #ifdef SDR_TIMING_BUILD
