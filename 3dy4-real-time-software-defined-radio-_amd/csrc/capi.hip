@@ -1278,8 +1278,9 @@ int sdr_stereo_front_u8_dev(sdr_ctx* c, const uint8_t* iq, long long iq_stride, 
 }
 
 // PLL recurrence (:123-126): the block's oscillator arguments into the work.
-// (A three-stage split -- recurrence | post stage on a third context -- was
-// measured slower than two stages and is not part of the ABI)
+// (A three-context split -- recurrence | post stage on a third context's
+// stream -- measured slower than two stages in round 5; the
+// halves are exported again for the two-stream schedule below.)
 static int stereo_pll(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_stereo_work* w) {
   if (!st || !w) return fail(c, SDR_EINVAL, "null state / work");
   hipError_t e = sdr::launch_pll_recurrence(w->pilot, w->nd, w->nstreams, w->dstride, 19e3f, audio_fs, 2.0f, 0.0f,
@@ -1316,6 +1317,35 @@ int sdr_stereo_back_dev(sdr_ctx* c, float audio_fs, const sdr_stereo_taps* taps,
   rc = stereo_pll(c, audio_fs, st, w);
   if (!rc) rc = stereo_post(c, taps, st, w, pcm, pcm_stride);
   const hipError_t e = w->uses.mark(c->cur);  // marked even after a failed launch
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  return SDR_OK;
+}
+
+// The back stage in its two halves, for a schedule that keeps the second
+// context's stream on the recurrences alone: block b's post stage (NCO,
+// stereo resampler, PCM) runs on the front stream after block b+1's front
+// stage, beside block b+1's recurrence (bench.py --stereo-pipeline 2).  The
+// post stage waits for its block's recurrence (the caller's event); the
+// stereo resampler state is the post stage's, the PLL state the recurrence's.
+int sdr_stereo_pll_dev(sdr_ctx* c, float audio_fs, sdr_stereo_state* st, sdr_stereo_work* w) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!st || !w) return fail(c, SDR_EINVAL, "null state / work");
+  rc = stereo_pll(c, audio_fs, st, w);
+  const hipError_t e = w->uses.mark(c->cur);  // marked even after a failed launch
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
+  return SDR_OK;
+}
+
+int sdr_stereo_post_dev(sdr_ctx* c, const sdr_stereo_taps* taps, sdr_stereo_state* st, sdr_stereo_work* w,
+                        int16_t* pcm, long long pcm_stride) {
+  int rc = enter(c);
+  if (rc) return rc;
+  if (!taps || !st || !w || !pcm) return fail(c, SDR_EINVAL, "null taps / state / work / pcm");
+  rc = stereo_post(c, taps, st, w, pcm, pcm_stride);
+  const hipError_t e = w->uses.mark(c->cur);
   if (rc) return rc;
   if (e != hipSuccess) return hip_fail(c, e, "hipEventRecord");
   return SDR_OK;

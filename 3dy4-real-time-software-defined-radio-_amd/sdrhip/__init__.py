@@ -114,6 +114,8 @@ _SIGS = {
     "sdr_stereo_work_destroy": [_vp, _vp],
     "sdr_stereo_front_u8_dev": [_vp, _vp, _ll, _vp, _vp, _vp],
     "sdr_stereo_back_dev": [_vp, C.c_float, _vp, _vp, _vp, _vp, _ll],
+    "sdr_stereo_pll_dev": [_vp, C.c_float, _vp, _vp],
+    "sdr_stereo_post_dev": [_vp, _vp, _vp, _vp, _vp, _ll],
     "sdr_synth_fm_u8_dev": [_vp, _vp, _ll, _i, _ll, C.c_ulonglong],
     "sdr_u8_to_planar_dev": [_vp, _vp, _ll, _i, _ll, _vp, _vp, _ll],
     "sdr_mono_work_create": [_vp, _i, _ll, _i, _i, _i, _i, _vp, _i, _i, _vp, _i, _i, C.POINTER(_vp)],
@@ -600,6 +602,15 @@ class Context:
         """Back stage (PLL recurrence onwards, :123-132 + 304-314) from `work` to s16 L/R."""
         self._check(lib().sdr_stereo_back_dev(self._c, audio_fs, C.addressof(taps), C.addressof(state), work._w,
                                               _ptr(pcm), pcm_stride), "stereo_back_dev")
+
+    def stereo_pll_dev(self, audio_fs, state, work):
+        """The back stage's recurrence half (:123-126): the block's oscillator arguments into `work`."""
+        self._check(lib().sdr_stereo_pll_dev(self._c, audio_fs, C.addressof(state), work._w), "stereo_pll_dev")
+
+    def stereo_post_dev(self, taps, state, work, pcm, pcm_stride):
+        """The back stage's post half (:127-132 + 304-314): NCO x stereo band, resampler, s16 L/R."""
+        self._check(lib().sdr_stereo_post_dev(self._c, C.addressof(taps), C.addressof(state), work._w, _ptr(pcm),
+                                              pcm_stride), "stereo_post_dev")
 
     def mono_work(self, D, npairs, up, down, nstreams, ns_delay, h_rf, rf_taps, ns_rf, h_audio, audio_taps,
                   ns_audio) -> "MonoWork":

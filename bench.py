@@ -120,11 +120,13 @@ def parse(argv=None):
                     help="steps per replayed HIP graph (0: min(--steps, 100), so the timed window is one or a few "
                          "replays and the host's launch rate never bounds a short step)")
     ap.add_argument("--no-graph", action="store_true", help="launch every step directly")
-    ap.add_argument("--stereo-pipeline", type=int, choices=(0, 1),
-                    default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "1")),
+    ap.add_argument("--stereo-pipeline", type=int, choices=(-1, 0, 1, 2),
+                    default=int(os.environ.get("SDR_BENCH_STEREO_PIPE", "-1")),
                     help="stereo configs: 1 = each step as two stages on two contexts' streams (front end + band-pass "
-                         "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence; 0 = "
-                         "one call per step")
+                         "filters | PLL recurrence onwards), step b+1's front overlapping step b's recurrence; 2 = the "
+                         "second stream runs the recurrences alone, step b's post stage (NCO, stereo resampler, PCM) "
+                         "following step b+1's front stage on the first; 0 = one call per step; -1 (default) = 2 while "
+                         "the recurrence's waves fill at most a quarter of the CUs, else 1 (DESIGN.md 5.2)")
     ap.add_argument("--mono-pipeline", type=int, choices=(0, 1),
                     default=int(os.environ.get("SDR_BENCH_MONO_PIPE", "0")),
                     help="mono0: 1 = each step as two stages on two contexts' streams (front end | delay + audio "
@@ -412,6 +414,13 @@ class Job:
             self.bound = "valu"
         elif kind == "stereo_u8":
             D, up, down = cfg["D"], cfg["up"], cfg["down"]
+            if args.stereo_pipeline < 0:
+                # the split schedule moves the post stage onto the front stream: a win while the
+                # one-lane-per-stream recurrence leaves the chip mostly idle (stereo0: 16 waves,
+                # -3.3 %), a loss once the front stage is as long as the recurrence (stereo0w:
+                # 256 waves, +15 %; profiles/r06ae/) -- the stereo call's own fork rule
+                cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                args.stereo_pipeline = 2 if (S + 63) // 64 <= cus // 4 else 1
             na = sdrhip.resample_out_len(up, down, n // D)
             z = lambda k: torch.zeros(S * k, dtype=torch.float32, device=dev)  # noqa: E731
             sbuf = dict(delay=z(50), audio=z(100), slp=z(100), pilot=z(100), stereo=z(100),
@@ -452,6 +461,30 @@ class Job:
                         ev_b[slot].record(ctx2)
                     if k:
                         ev_b[(j0 + k - 1) % nslot].wait(ctx)
+                if args.stereo_pipeline == 2:
+                    ev_p = [sdrhip.Event(ctx) for _ in range(nslot)]
+                    self.keep.append(ev_p)
+
+                    def seq(j0, k):  # noqa: F811
+                        """k consecutive steps, the recurrences alone on the second stream:
+                        front(b) and then post(b-1) (after recurrence b-1) on this stream,
+                        recurrence b (after front b) on the second.  A slot's work is free
+                        again when post(b-2) -- earlier on this stream -- has run."""
+                        for j in range(k):
+                            slot = (j0 + j) % nslot
+                            ctx.stereo_front_u8_dev(iqs[(j0 + j) % len(iqs)], 2 * n, taps_s, state_s, works[slot])
+                            ev_f[slot].record(ctx)
+                            ev_f[slot].wait(ctx2)
+                            ctx2.stereo_pll_dev(240e3, state_s, works[slot])
+                            ev_p[slot].record(ctx2)
+                            if j:
+                                prev = (slot - 1) % nslot
+                                ev_p[prev].wait(ctx)
+                                ctx.stereo_post_dev(taps_s, state_s, works[prev], pcm, 2 * na)
+                        if k:
+                            last = (j0 + k - 1) % nslot
+                            ev_p[last].wait(ctx)
+                            ctx.stereo_post_dev(taps_s, state_s, works[last], pcm, 2 * na)
                 self.seq = seq
             for iq in iqs:
                 steps.append(lambda iq=iq: ctx.stereo_pcm_u8_dev(D, iq, n, S, 2 * n, up, down, 240e3, taps_s,
@@ -877,9 +910,13 @@ def main(argv=None):
                        "devices_opened": distinct, "input_batches": max(1, args.batches),
                        "launch": "direct" if args.no_graph else
                                  f"HIP graph of {args.graph_steps or min(max(args.steps, 1), 100)} steps",
-                       **({"stereo_pipeline": ("two stages on two contexts' streams (front | PLL onwards), step "
-                                               "b+1's front overlapping step b's recurrence")
-                           if args.stereo_pipeline else "one call per step"} if job["kind"] == "stereo_u8" else {}),
+                       **({"stereo_pipeline": {0: "one call per step",
+                                               1: "two stages on two contexts' streams (front | PLL onwards), step "
+                                                  "b+1's front overlapping step b's recurrence",
+                                               2: "recurrences alone on a second context's stream; step b's post "
+                                                  "stage (NCO, stereo resampler, PCM) after step b+1's front stage "
+                                                  "on the first"}[args.stereo_pipeline]}
+                          if job["kind"] == "stereo_u8" else {}),
                        **({"mono_pipeline": ("two stages on two contexts' streams (front end | delay + audio filter "
                                              "+ PCM), step b+1's front end beside step b's audio stage")
                            if args.mono_pipeline else "one call per step"} if job["kind"] == "mono_u8" else {}),

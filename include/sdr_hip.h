@@ -63,7 +63,8 @@ typedef struct sdr_ctx sdr_ctx;
  *   2  round 5: the three-stage stereo split (sdr_stereo_pll_dev /
  *      sdr_stereo_post_dev) removed; switch table (sdr_set_switch)
  *   3  round 6: sdr_libm_* verification entry points, the two-stage mono
- *      path (sdr_mono_work_*, sdr_mono_front_u8_dev, sdr_mono_back_dev) */
+ *      path (sdr_mono_work_*, sdr_mono_front_u8_dev, sdr_mono_back_dev), the
+ *      stereo back stage's halves (sdr_stereo_pll_dev, sdr_stereo_post_dev) */
 #define SDR_ABI_VERSION 3
 int sdr_abi_version(void);
 
@@ -366,6 +367,15 @@ int sdr_stereo_front_u8_dev(sdr_ctx *ctx, const uint8_t *iq, long long iq_stride
                             sdr_stereo_state *state, sdr_stereo_work *work);
 int sdr_stereo_back_dev(sdr_ctx *ctx, float audio_fs, const sdr_stereo_taps *taps, sdr_stereo_state *state,
                         sdr_stereo_work *work, int16_t *pcm, long long pcm_stride);
+/* The back stage's two halves: the recurrence (PLL state) and the post stage
+ * (NCO x stereo band, stereo resampler, L/R s16; the stereo resampler state),
+ * so block b's post stage can run on the front stage's stream after block
+ * b+1's front stage while block b+1's recurrence runs on the back stream
+ * (the caller orders post(b) after pll(b) with an sdr_event).  Together they
+ * equal sdr_stereo_back_dev. */
+int sdr_stereo_pll_dev(sdr_ctx *ctx, float audio_fs, sdr_stereo_state *state, sdr_stereo_work *work);
+int sdr_stereo_post_dev(sdr_ctx *ctx, const sdr_stereo_taps *taps, sdr_stereo_state *state, sdr_stereo_work *work,
+                        int16_t *pcm, long long pcm_stride);
 
 /* The mono path in two stages (like the stereo pair above): sdr_mono_front_u8_dev
  * runs the RF front end of one block into the work's row (src/project.cpp:72-93);

@@ -340,15 +340,21 @@ def test_long_stream_segments_two_threads(built_lib, oracle, D, T, ns):
     assert_bits(res[1][3], pv, "prev vs the oracle")
 
 
+@pytest.mark.parametrize("sched", ["back", "split"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
-    """bench.py --stereo-pipeline's schedule (and sdr_project's): each block as
-    sdr_stereo_front_u8_dev on one context's stream and sdr_stereo_back_dev on
-    a second context's, two work objects in a ring, front(b) waiting for
+def test_stereo_two_stage_pipeline(built_lib, oracle, graph, sched):
+    """bench.py --stereo-pipeline's schedules (and sdr_project's): each block as
+    sdr_stereo_front_u8_dev on one context's stream and the back stage on a
+    second context's, two work objects in a ring.
+    back (--stereo-pipeline 1): sdr_stereo_back_dev, front(b) waiting for
     back(b-2) and back(b) for front(b) by sdr_ctx_wait_event -- block b+1's
-    front overlapping block b's PLL recurrence.  128 streams x 5 mode-0
-    blocks, direct or captured as one HIP graph spanning both streams:
-    every PCM byte and every carried state word against the oracle chain."""
+    front overlapping block b's PLL recurrence.
+    split (--stereo-pipeline 2): sdr_stereo_pll_dev alone on the second
+    stream, block b's sdr_stereo_post_dev on the first after block b+1's
+    front stage and block b's recurrence.
+    128 streams x 5 mode-0 blocks, direct or captured as one HIP graph
+    spanning both streams: every PCM byte and every carried state word
+    against the oracle chain."""
     sdrhip = built_lib
     mode, nstreams, nblk = 0, 128, 5
     rf_fs, D, audio_fs, up, down, block_bytes, taps = _stereo_setup(oracle, mode)
@@ -374,6 +380,20 @@ def test_stereo_two_stage_pipeline(built_lib, oracle, graph):
         ev_b = [sdrhip.Event(ca) for _ in range(ns_)]
 
         def run(b0, k):
+            if sched == "split":
+                for j in range(k):
+                    b, slot = b0 + j, (b0 + j) % ns_
+                    ca.stereo_front_u8_dev(blocks[b][0], 2 * npairs, t, state, works[slot])
+                    ev_f[slot].record(ca)
+                    ev_f[slot].wait(cb)
+                    cb.stereo_pll_dev(audio_fs, state, works[slot])
+                    ev_b[slot].record(cb)
+                    if j:
+                        ev_b[(slot - 1) % ns_].wait(ca)
+                        ca.stereo_post_dev(t, state, works[(slot - 1) % ns_], pcm[b - 1], 2 * na)
+                ev_b[(b0 + k - 1) % ns_].wait(ca)
+                ca.stereo_post_dev(t, state, works[(b0 + k - 1) % ns_], pcm[b0 + k - 1], 2 * na)
+                return
             for j in range(k):
                 b, slot = b0 + j, (b0 + j) % ns_
                 if j >= ns_:
