@@ -206,18 +206,28 @@ int main(int argc, char* argv[]) {
   // (DESIGN.md 4.7).  Each ring slot has its own work object; front(b) waits for
   // back(b-2) (the slot's previous user), back(b) for front(b).  SDR_PROJECT_SPLIT=0
   // runs the whole block as one call instead.
+  // SDR_PROJECT_SPLIT=2 (the default) keeps the second stream on the recurrences alone:
+  // block b's post stage (NCO, stereo resampler, PCM, copy-out) runs on g_ctx's stream
+  // after block b+1's front stage, once recurrence b is done (sdr_stereo_pll_dev /
+  // sdr_stereo_post_dev; bench.py --stereo-pipeline 2).  Its PCM then leaves one block
+  // later than under SPLIT=1, which is when the loop below writes it out anyway.
   const char* spl = std::getenv("SDR_PROJECT_SPLIT");
   // mode-0 stereo, 3,000 blocks: 3.358 s split vs 3.560 s one call (profiles/r04e/ab.txt)
-  const bool split = !mono && !(spl && std::atoi(spl) == 0);
+  const int split_mode = mono ? 0 : (spl ? std::atoi(spl) : 2);
+  const bool split = split_mode != 0;
+  const bool post_front = split_mode == 2;
   sdr_ctx* g_back = nullptr;
   sdr_stereo_work* work[2] = {nullptr, nullptr};
   sdr_event* front_done[2] = {nullptr, nullptr};
+  sdr_event* pll_done[2] = {nullptr, nullptr};
   sdr_graph* graph_back[2] = {nullptr, nullptr};
+  sdr_graph* graph_post[2] = {nullptr, nullptr};
   if (split) {
     check(sdr_ctx_create(devenv ? std::atoi(devenv) : 0, &g_back), "ctx_create");
     for (int i = 0; i < 2; ++i) {
       check(sdr_stereo_work_create(g_ctx, rf_decim, npairs, audio_up, audio_decim, 1, &work[i]), "stereo_work_create");
       check(sdr_event_create(g_ctx, &front_done[i]), "event_create");
+      check(sdr_event_create(g_ctx, &pll_done[i]), "event_create");
     }
   }
   auto enqueue_front = [&](int k) {
@@ -226,9 +236,18 @@ int main(int argc, char* argv[]) {
           "stereo_front_u8_dev");
   };
   auto enqueue_back = [&](int k) {
+    if (post_front) {
+      check(sdr_stereo_pll_dev(g_back, audio_Fs, &st, work[k]), "stereo_pll_dev");
+      return;
+    }
     check(sdr_stereo_back_dev(g_back, audio_Fs, &taps, &st, work[k], static_cast<int16_t*>(d_out[k]), pcm_len),
           "stereo_back_dev");
     check(sdr_copy_d2h_async(g_back, h_out[k], d_out[k], pcm_len * sizeof(int16_t)), "copy_d2h_async");
+  };
+  auto enqueue_post = [&](int k) {  // SPLIT=2: on g_ctx, after recurrence k
+    check(sdr_stereo_post_dev(g_ctx, &taps, &st, work[k], static_cast<int16_t*>(d_out[k]), pcm_len),
+          "stereo_post_dev");
+    check(sdr_copy_d2h_async(g_ctx, h_out[k], d_out[k], pcm_len * sizeof(int16_t)), "copy_d2h_async");
   };
   // run f on ctx directly (block 0 sizes the scratch) or as slot k's recorded graph
   auto run = [&](sdr_ctx* ctx, sdr_graph** g, bool direct, auto&& f) {
@@ -249,11 +268,20 @@ int main(int argc, char* argv[]) {
     std::fwrite(h_out[b & 1], sizeof(int16_t), pcm_len, stdout);
   };
 
+  // SPLIT=2: block b's post stage, after its recurrence (the first one sizes its scratch)
+  auto post = [&](unsigned b) {
+    const int j = b & 1;
+    check(sdr_ctx_wait_event(g_ctx, pll_done[j]), "wait_event");
+    run(g_ctx, &graph_post[j], b == 0 || !use_graph, [&] { enqueue_post(j); });
+    check(sdr_event_record(g_ctx, done[j]), "event_record");
+  };
+
   for (unsigned int block_id = 0;; block_id++) {
     std::cerr << "Block number " << block_id << std::endl;
     const int k = block_id & 1;
     // h_in[k] was last used by block_id - 2, whose copy finished before flush(block_id - 2)
     if (read_full(h_in[k], block_size) != (size_t)block_size) {
+      if (post_front && block_id > 0) post(block_id - 1);
       if (block_id > 0) flush(block_id - 1);
       std::fflush(stdout);
       std::cerr << "End of input stream reached" << std::endl;
@@ -263,12 +291,14 @@ int main(int argc, char* argv[]) {
     // inside a capture); then each ring slot's sequence is recorded once and replayed
     const bool direct = block_id == 0 || !use_graph;
     if (split) {
-      if (block_id >= 2) check(sdr_ctx_wait_event(g_ctx, done[k]), "wait_event");  // back(b-2) released work[k]
+      // back(b-2) released work[k] (SPLIT=2: post(b-2), earlier on this stream)
+      if (block_id >= 2 && !post_front) check(sdr_ctx_wait_event(g_ctx, done[k]), "wait_event");
       run(g_ctx, &graph[k], direct, [&] { enqueue_front(k); });
       check(sdr_event_record(g_ctx, front_done[k]), "event_record");
       check(sdr_ctx_wait_event(g_back, front_done[k]), "wait_event");
       run(g_back, &graph_back[k], direct, [&] { enqueue_back(k); });
-      check(sdr_event_record(g_back, done[k]), "event_record");
+      check(sdr_event_record(g_back, post_front ? pll_done[k] : done[k]), "event_record");
+      if (post_front && block_id > 0) post(block_id - 1);
     } else {
       run(g_ctx, &graph[k], direct, [&] { enqueue(k); });
       check(sdr_event_record(g_ctx, done[k]), "event_record");

@@ -19,12 +19,15 @@ fs = {0: 2.4e6, 1: 1.44e6, 2: 2.4e6, 3: 1.92e6}[mode]
 fm_iq_u8(bb * nblk // 2, seed=5, fs=fs).tofile(path)
 PY
   for ch in mono stereo; do
-    for v in ref graph direct onecall; do
+    for v in ref graph graph1 direct onecall; do
       [ $v = onecall ] && [ $ch = mono ] && continue
+      [ $v = graph1 ] && [ $ch = mono ] && continue
       case $v in
         ref) prog=oracle/_ref/project_ref; env=;;
-        graph) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=0 SDR_PROJECT_SPLIT=1";;
-        direct) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=1 SDR_PROJECT_SPLIT=1";;
+        graph) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=0 SDR_PROJECT_SPLIT=2";;
+        # the whole back stage on the second stream (the round-4 schedule)
+        graph1) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=0 SDR_PROJECT_SPLIT=1";;
+        direct) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env="SDR_PROJECT_NO_GRAPH=1 SDR_PROJECT_SPLIT=2";;
         # stereo as one call per block (no overlap of block b+1's front with block b's PLL)
         onecall) prog=3dy4-real-time-software-defined-radio-_amd/sdr_project; env=SDR_PROJECT_SPLIT=0;;
       esac

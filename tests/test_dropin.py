@@ -121,7 +121,7 @@ def test_reference_project_on_dropin(gpu_ctx, mode, channel):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
-@pytest.mark.parametrize("channel", ["mono", "stereo", "stereo-onecall"])
+@pytest.mark.parametrize("channel", ["mono", "stereo", "stereo-back", "stereo-onecall"])
 def test_sdr_project_program(built_lib, oracle, mode, channel):
     """host/sdr_project: src/project.cpp's program with the device block
     pipeline (pinned ring, one stream-ordered call per block).  Same stdout
@@ -130,13 +130,16 @@ def test_sdr_project_program(built_lib, oracle, mode, channel):
     on 5.5 blocks of input: the trailing partial block is dropped and the
     exit status is 1, as src/project.cpp:293-297 does.  Stereo runs each block
     as two stages on two contexts' streams, block b+1's front overlapping
-    block b's PLL recurrence (and the ring slots reused: 5 blocks, 2 slots);
-    stereo-onecall is the one-call form (SDR_PROJECT_SPLIT=0)."""
+    block b's PLL recurrence (and the ring slots reused: 5 blocks, 2 slots):
+    by default the second stream runs the recurrences alone and block b's
+    post stage follows block b+1's front stage (SDR_PROJECT_SPLIT=2);
+    stereo-back runs the whole back stage on the second stream
+    (SDR_PROJECT_SPLIT=1); stereo-onecall is the one-call form (=0)."""
     prog = os.path.join(REPO, "3dy4-real-time-software-defined-radio-_amd", "sdr_project")
     assert os.path.exists(prog), "sdr_project not built"
     from sdrhip.synth import fm_iq_u8
 
-    env = dict(os.environ, SDR_PROJECT_SPLIT="0" if channel == "stereo-onecall" else "1")
+    env = dict(os.environ, SDR_PROJECT_SPLIT={"stereo-onecall": "0", "stereo-back": "1"}.get(channel, "2"))
     channel = channel.split("-")[0]
     block_bytes = MODES[mode][5]
     fs = MODES[mode][0]
