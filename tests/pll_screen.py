@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "3dy4-real-time-software-
 FS, F0, NCO_SCALE, PHASE_ADJ, NORM_BW = 240e3, 19e3, 2.0, 0.0, 0.01
 
 
-def screen(ctx, streams: int, blocks: int, n: int = 5120, seed: int = 1, progress=None) -> dict:
+def screen(ctx, streams: int, blocks: int, n: int = 5120, seed: int = 1, progress=None, fs: float = FS) -> dict:
     import torch
 
     import sdrhip
@@ -65,7 +65,7 @@ def screen(ctx, streams: int, blocks: int, n: int = 5120, seed: int = 1, progres
     try:
         for b in range(blocks):
             t = torch.arange(b * n, (b + 1) * n, device=dev, dtype=torch.float64)[None, :]
-            x = amp * torch.cos(2 * math.pi * f / FS * t + phi) + noise * torch.randn(
+            x = amp * torch.cos(2 * math.pi * f / fs * t + phi) + noise * torch.randn(
                 (streams, n), generator=g, device=dev, dtype=torch.float64)
             zeros = (kind == 0) & (torch.rand((streams, n), generator=g, device=dev) < 0.01)
             x = torch.where(zeros, torch.zeros_like(x), x)
@@ -76,7 +76,7 @@ def screen(ctx, streams: int, blocks: int, n: int = 5120, seed: int = 1, progres
             for fast in ("1", "0"):
                 sdrhip.set_switch("SDR_PLL_FAST", int(fast))
                 c0 = time.time()
-                ctx.fm_pll_dev(x, n, streams, n, F0, FS, NCO_SCALE, PHASE_ADJ, NORM_BW, st[fast], None, n, out[fast], n)
+                ctx.fm_pll_dev(x, n, streams, n, F0, fs, NCO_SCALE, PHASE_ADJ, NORM_BW, st[fast], None, n, out[fast], n)
                 ctx.synchronize()
                 dt[fast] += time.time() - c0
             mism_out += int((out["1"].view(torch.int32) != out["0"].view(torch.int32)).sum())
@@ -86,7 +86,7 @@ def screen(ctx, streams: int, blocks: int, n: int = 5120, seed: int = 1, progres
     finally:
         sdrhip.set_switch("SDR_PLL_FAST", 1)
     trig = st["1"][:, 4]
-    return {"streams": streams, "blocks": blocks, "samples_per_block": n, "seed": seed,
+    return {"streams": streams, "blocks": blocks, "samples_per_block": n, "seed": seed, "fs": fs,
             "pll_steps": streams * n * blocks, "output_mismatches": mism_out, "state_mismatches": mism_state,
             "trigoffset_max": float(trig.max()), "streams_at_2p24": int((trig >= 16777216.0).sum()),
             "seconds_fast": round(dt["1"], 3), "seconds_library": round(dt["0"], 3),
@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=200)
     ap.add_argument("--n", type=int, default=5120)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--fs", type=float, default=FS,
+                    help="the PLL's sample rate: the IF rate of the reference's modes (0/2: 240e3, 1: 288e3, 3: 384e3)")
     a = ap.parse_args()
     import torch
 
@@ -110,7 +112,7 @@ def main():
     def progress(b, mo, ms):
         print(f"block {b}/{a.blocks}: mismatches {mo} outputs, {ms} state words", file=sys.stderr, flush=True)
 
-    print(json.dumps(screen(ctx, a.streams, a.blocks, a.n, a.seed, progress)), flush=True)
+    print(json.dumps(screen(ctx, a.streams, a.blocks, a.n, a.seed, progress, a.fs)), flush=True)
 
 
 if __name__ == "__main__":
